@@ -1,0 +1,303 @@
+"""CPU oracle: a NumPy restatement of the reference's timing-metric + CFO hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the checker
+(or as the timed CPU baseline).  The product path (``ofdm-sync-math_amd/``) never
+imports it and has no CPU fallback.
+
+Parity pinning: every function here is checked against golden vectors produced by the
+reference itself (``tests/golden/make_golden.py`` imports /root/reference and runs it)
+and against the reference's own fixtures ``docs/detector_test_vector.csv`` /
+``docs/detector_cfo_test_vector.csv`` (tests/test_oracle_golden.py).
+
+The restatement is written in prefix-sum form (float64 ``cumsum``) rather than the
+reference's per-sample recursion; for float inputs the two agree to ~1e-12 relative,
+for integer-valued inputs (int12 ADC samples) they are bit-identical because every
+partial sum is an exactly representable integer (< 2**53).  The gate/peak state
+machines are restated as literal loops, statement for statement.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+__all__ = [
+    "aa_metric", "aa_events", "aa_detect",
+    "sc_metric", "comb_sc_metric", "minn_metric",
+    "minn_rtl_metric", "detect_minn_rtl", "cp_cfo",
+]
+
+
+def _as2d(x, dtype=np.complex128):
+    x = np.asarray(x)
+    if x.ndim == 1:
+        x = x[np.newaxis, :]
+    return x.astype(dtype, copy=False)
+
+
+def _pref(v):
+    """Exclusive-at-zero prefix: p[i+1] = sum(v[:i+1]); p[0] = 0."""
+    out = np.zeros(v.shape[:-1] + (v.shape[-1] + 1,), dtype=v.dtype)
+    np.cumsum(v, axis=-1, out=out[..., 1:])
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# sync_aa.aa_detect_streaming  (sync_aa.py:421-571)
+# ---------------------------------------------------------------------------------------
+def aa_metric(rx, L):
+    """P[n], R[n], M[n], valid[n] of sync_aa.aa_detect_streaming (sync_aa.py:458-493).
+
+    product[j] = x[j]*conj(x[j-L]) for j >= L, else 0          (DelayLine, :377-386, :466-469)
+    P[n] = sum_{j=n-L+1..n} product[j] (window clipped at 0)      (RunningSum, :331-342)
+    R[n] = sum_{j=n-L+1..n} |x[j]|^2                               (RunningSumReal, :355-365)
+    valid[n] = n >= L                                              (filled == L, :338-342)
+    M = min(|P|^2/R^2, 1) if valid and R > 1e-6*L else 0           (:486-493)
+    """
+    x = _as2d(rx)
+    _, T = x.shape
+    prod = np.zeros_like(x)
+    if T > L:
+        prod[:, L:] = x[:, L:] * np.conj(x[:, :-L])
+    e = (x.real ** 2 + x.imag ** 2)
+    Pp = _pref(prod.sum(axis=0))
+    Ep = _pref(e.sum(axis=0))
+    n = np.arange(T)
+    lo = np.maximum(n - L + 1, 0)
+    P = Pp[n + 1] - Pp[lo]
+    R = Ep[n + 1] - Ep[lo]
+    valid = n >= L
+    M = np.zeros(T)
+    ok = valid & (R > 1e-6 * L)
+    M[ok] = np.minimum((np.abs(P[ok]) ** 2) / (R[ok] ** 2), 1.0)
+    return P, R, M, valid
+
+
+def aa_events(P, M, valid, L, threshold=0.15, hysteresis=128, sample_rate=15.36e6):
+    """Gate/peak/CFO state machine, literal restatement of sync_aa.py:495-568.
+
+    Returns (ints[k,4] = peak_index, gate_start, gate_end, frame_start,
+             reals[k,4] = P_re, P_im, M_at_peak, cfo_hz).
+    """
+    T = len(M)
+    ints, reals = [], []
+    gate_open = False
+    gate_start = peak_index = low_count = 0
+    peak_P = 0j
+    peak_mag = 0.0
+
+    def emit(end):
+        cfo = np.angle(peak_P) * sample_rate / (2 * np.pi * L)
+        ints.append((peak_index, gate_start, end, peak_index - 2 * L + 1))
+        reals.append((peak_P.real, peak_P.imag, M[peak_index], cfo))
+
+    for n in range(T):
+        if not valid[n]:
+            continue
+        m = M[n]
+        pm = np.abs(P[n]) ** 2
+        if not gate_open:
+            if m >= threshold:
+                gate_open, gate_start, peak_index, peak_P, peak_mag, low_count = True, n, n, P[n], pm, 0
+        else:
+            if pm > peak_mag:
+                peak_index, peak_P, peak_mag = n, P[n], pm
+            if m >= threshold:
+                low_count = 0
+            else:
+                low_count += 1
+                if low_count >= hysteresis:
+                    emit(n)
+                    gate_open, peak_mag, low_count = False, 0.0, 0
+    if gate_open:
+        emit(T)
+    return (np.array(ints, dtype=np.int64).reshape(-1, 4),
+            np.array(reals, dtype=np.float64).reshape(-1, 4))
+
+
+def aa_detect(rx, L=512, threshold=0.15, hysteresis=128, sample_rate=15.36e6):
+    P, R, M, valid = aa_metric(rx, L)
+    ints, reals = aa_events(P, M, valid, L, threshold, hysteresis, sample_rate)
+    return P, R, M, valid, ints, reals
+
+
+# ---------------------------------------------------------------------------------------
+# sc.sc_streaming_metric (sc.py:42-78) and combined_sc_min.schmidl_cox_streaming_metric
+# (combined_sc_min.py:116-164)
+# ---------------------------------------------------------------------------------------
+def _sc_common(rx, N, both_halves):
+    x = _as2d(rx)
+    _, T = x.shape
+    half = N // 2
+    out_len = T - N + 1
+    if half == 0 or out_len <= 0:
+        return np.zeros(0), np.zeros(0, np.complex128), np.zeros(0)
+    if N != 2 * half:
+        raise ValueError("symbol length must be even (halves of equal length)")
+    # P(d) = sum_{k<half} x[d+k] conj(x[d+half+k])
+    prod = (x[:, :-half] * np.conj(x[:, half:])).sum(axis=0)          # index j = d+k
+    Pp = _pref(prod)
+    Ep = _pref((x.real ** 2 + x.imag ** 2).sum(axis=0))
+    d = np.arange(out_len)
+    P = Pp[d + half] - Pp[d]
+    if both_halves:
+        R = Ep[d + N] - Ep[d]                                         # combined_sc_min.py:154
+    else:
+        R = Ep[d + N] - Ep[d + half]                                  # sc.py:61
+    M = (np.abs(P) ** 2) / (np.maximum(R, 1e-12) ** 2)
+    return M, P, R
+
+
+def sc_metric(rx, N):
+    """sc.sc_streaming_metric with sc.N_FFT == N (sc.py:42-78)."""
+    return _sc_common(rx, N, both_halves=False)
+
+
+def comb_sc_metric(rx, N):
+    """combined_sc_min.schmidl_cox_streaming_metric(rx, symbol_len=N) (combined_sc_min.py:116-164)."""
+    return _sc_common(rx, N, both_halves=True)
+
+
+# ---------------------------------------------------------------------------------------
+# Minn metric: minn.minn_streaming_metric (minn.py:59-112), _parameterized (minn.py:697-751),
+# combined_sc_min.minn_streaming_metric (combined_sc_min.py:60-113)
+# ---------------------------------------------------------------------------------------
+def minn_metric(rx, N):
+    x = _as2d(rx)
+    _, T = x.shape
+    Q = N // 4
+    out_len = T - N + 1
+    if out_len <= 0:
+        return np.zeros(0), np.zeros(0, np.complex128), np.zeros(0)
+    if Q == 0:
+        z = np.zeros(out_len)
+        return z, np.zeros(out_len, np.complex128), z.copy()
+    # C(d) = sum_{k<Q} x[d+k] conj(x[d+Q+k]);  P = C(d) + C(d+2Q)
+    prod = (x[:, :-Q] * np.conj(x[:, Q:])).sum(axis=0)
+    Cp = _pref(prod)
+    Ep = _pref((x.real ** 2 + x.imag ** 2).sum(axis=0))
+    d = np.arange(out_len)
+    P = (Cp[d + Q] - Cp[d]) + (Cp[d + 3 * Q] - Cp[d + 2 * Q])
+    R = Ep[d + 4 * Q] - Ep[d + Q]
+    M = np.clip(P.real, 0.0, None) ** 2 / (np.maximum(R, 1e-12) ** 2)
+    return M, P, R
+
+
+# ---------------------------------------------------------------------------------------
+# minn_rtl.minn_rtl_streaming_metric (minn_rtl.py:667-733) + detect_minn_rtl (:750-825)
+# ---------------------------------------------------------------------------------------
+def minn_rtl_metric(rx, Q, smooth_shift, threshold_value, threshold_frac_bits, smooth_mode="float"):
+    """Closed form of the _antenna_path pipeline (minn_rtl.py:583-652), summed over branches.
+
+    prod[j] = Re(x[j] conj(x[j-Q])) for j >= Q else 0     (_DelayLine fill phase, :524-542)
+    C[i] = sum_{j=i-Q+1..i} prod[j];  E[i] = sum |x[j]|^2   (_RunningSum, :558-580)
+    corr_recent = C[i]   (i >= Q-1), corr_previous = C[i-Q]   (i >= 2Q-1)
+    energy: E[i] (i >= Q-1), E[i-Q] (i >= 2Q-1), E[i-2Q] (i >= 3Q-1); registers hold 0 before
+    taps_valid = i >= 3Q-1.
+    smooth_mode "float": the float64 IIR of minn_rtl.py:706-715 (bit-exact restatement);
+    "floor": the integer floor-shift IIR of ref/minn_preamble_detector.sv:288-296.
+    """
+    x = _as2d(rx)
+    _, T = x.shape
+    if Q <= 0:
+        raise ValueError("quarter_len must be positive.")
+    prod = np.zeros(x.shape)
+    if T > Q:
+        prod[:, Q:] = x[:, :-Q].real * x[:, Q:].real + x[:, :-Q].imag * x[:, Q:].imag
+    pw = x.real * x.real + x.imag * x.imag
+    Cp = _pref(prod.sum(axis=0))
+    Ep = _pref(pw.sum(axis=0))
+    i = np.arange(T)
+    lo = np.maximum(i - Q + 1, 0)
+    C = Cp[i + 1] - Cp[lo]
+    E = Ep[i + 1] - Ep[lo]
+
+    def delayed(a, k, start):
+        out = np.zeros(T)
+        m = i >= start
+        out[m] = a[i[m] - k]
+        return out
+
+    corr_total = delayed(C, 0, Q - 1) + delayed(C, Q, 2 * Q - 1)
+    energy_total = delayed(E, 0, Q - 1) + delayed(E, Q, 2 * Q - 1) + delayed(E, 2 * Q, 3 * Q - 1)
+    valid = i >= 3 * Q - 1
+    corr_positive = np.maximum(corr_total, 0.0)
+    smooth = np.zeros(T)
+    s = 0.0
+    if smooth_mode == "float":
+        denom = 1 << max(0, smooth_shift)
+        for k in range(T):
+            if valid[k]:
+                if smooth_shift == 0:
+                    s = corr_positive[k]
+                else:
+                    s += (corr_positive[k] - s) / denom
+            smooth[k] = s
+    elif smooth_mode == "floor":
+        si = 0
+        cpi = corr_positive.astype(np.int64)
+        for k in range(T):
+            if valid[k]:
+                si = int(cpi[k]) if smooth_shift == 0 else si + ((int(cpi[k]) - si) >> smooth_shift)
+            smooth[k] = si
+    else:
+        raise ValueError(smooth_mode)
+    corr_scaled = smooth * (1 << threshold_frac_bits)
+    energy_scaled = np.zeros(T) if threshold_value == 0 else energy_total * float(threshold_value)
+    above = valid & (corr_scaled >= energy_scaled)
+    return dict(corr_total=corr_total, corr_positive=corr_positive, smooth_metric=smooth,
+                energy_total=energy_total, corr_scaled=corr_scaled, energy_scaled=energy_scaled,
+                metric_valid=valid, above_threshold=above)
+
+
+def detect_minn_rtl(corr_positive, above, valid, hysteresis, timing_offset):
+    """Literal restatement of minn_rtl.detect_minn_rtl (minn_rtl.py:750-825).
+
+    Returns (events[k,4] = peak_index, detected_index, seg_start, seg_end,
+             segments[s,2], gate_mask).
+    """
+    T = len(corr_positive)
+    segs, evs = [], []
+    gate_open = False
+    gate_start = None
+    peak_value = 0.0
+    peak_index = low = 0
+    hyst_limit = hysteresis - 1 if hysteresis > 0 else 0
+    for idx in range(T):
+        if not valid[idx]:
+            continue
+        v = corr_positive[idx]
+        if not gate_open:
+            if above[idx]:
+                gate_open, gate_start, peak_value, peak_index, low = True, idx, v, idx, 0
+        else:
+            if v >= peak_value:
+                peak_value, peak_index = v, idx
+            if above[idx]:
+                low = 0
+            else:
+                closing = hysteresis == 0 or low == hyst_limit
+                if not closing:
+                    low += 1
+                if closing:
+                    seg = (gate_start if gate_start is not None else idx, idx + 1)
+                    segs.append(seg)
+                    evs.append((peak_index, peak_index + timing_offset, seg[0], seg[1]))
+                    gate_open, gate_start, peak_value, low = False, None, 0.0, 0
+    if gate_open and gate_start is not None:
+        segs.append((gate_start, T))
+    mask = np.zeros(T, dtype=bool)
+    for a, b in segs:
+        mask[a:b] = True
+    return (np.array(evs, dtype=np.int64).reshape(-1, 4),
+            np.array(segs, dtype=np.int64).reshape(-1, 2), mask)
+
+
+# ---------------------------------------------------------------------------------------
+# core.estimate_cfo_from_cp (core.py:179-196)
+# ---------------------------------------------------------------------------------------
+def cp_cfo(rx, start, n_fft, cp_len, fs_hz):
+    x = _as2d(rx)
+    a = x[:, start:start + cp_len]
+    b = x[:, start + n_fft:start + n_fft + cp_len]
+    P = np.sum(a * np.conj(b))
+    return float(-np.angle(P) * fs_hz / (2 * np.pi * n_fft)), complex(P)

@@ -1,0 +1,256 @@
+"""Generate golden input/output fixtures from the reference (amcolex/ofdm-sync-math).
+
+TEST INFRASTRUCTURE ONLY.  This script imports the read-only reference checkout at
+``/root/reference`` (pure Python/NumPy) and runs its hot-path functions on seeded
+inputs, writing *data* (inputs + expected outputs) to ``tests/golden/*.npz``.  The
+reference itself never leaves this container; only these vectors travel.
+
+Run (from anywhere):
+    PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
+
+Reference entry points exercised (file:line into /root/reference):
+  sync_aa.aa_detect_streaming          sync_aa.py:421-571
+  sc.sc_streaming_metric               sc.py:42-78        (sc.N_FFT overridden per case)
+  combined_sc_min.schmidl_cox_streaming_metric  combined_sc_min.py:116-164
+  combined_sc_min.minn_streaming_metric         combined_sc_min.py:60-113
+  minn.minn_streaming_metric_parameterized      minn.py:697-751
+  minn_rtl.minn_rtl_streaming_metric  minn_rtl.py:667-733
+  minn_rtl.detect_minn_rtl             minn_rtl.py:750-825
+  core.estimate_cfo_from_cp            core.py:179-196
+Input builders used only to synthesise realistic streams (not part of the parity surface):
+  sync_aa.build_aa_preamble / apply_channel_multi_antenna / apply_cfo / quantize_adc,
+  sc.build_sc_preamble, combined_sc_min.build_minn_preamble, minn_rtl.build_minn_preamble_generic,
+  channel.apply_channel / load_measured_cir, core.build_random_qpsk_symbol / apply_cfo.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+
+
+def _import_reference():
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, str(REF))
+    os.chdir(tempfile.mkdtemp(prefix="ofs_golden_"))  # scripts write plots/ relative to cwd
+    import core, channel, sc, minn, minn_rtl, combined_sc_min, sync_aa  # noqa: E401
+    return dict(core=core, channel=channel, sc=sc, minn=minn, minn_rtl=minn_rtl,
+                combined=combined_sc_min, sync_aa=sync_aa)
+
+
+def _events_aa(res):
+    ev = res.events
+    ints = np.array([[e.peak_index, e.gate_start, e.gate_end, e.frame_start] for e in ev],
+                    dtype=np.int64).reshape(-1, 4)
+    reals = np.array([[e.P_at_peak.real, e.P_at_peak.imag, e.M_at_peak, e.cfo_hz] for e in ev],
+                     dtype=np.float64).reshape(-1, 4)
+    return ints, reals
+
+
+def gen_aa(R, cases):
+    sa = R["sync_aa"]
+    pre1024 = sa.build_aa_preamble(1024)[0]
+    tx = np.concatenate([np.zeros(500, complex), pre1024, np.zeros(500, complex)])
+    # (1) the exact docs/detector_test_vector.csv input, and (2) its CFO variant
+    for name, x in (("aa_clean_L512", tx), ("aa_cfo_L512", sa.apply_cfo(tx, 500.0, 15.36e6))):
+        res = sa.aa_detect_streaming(x, L=512)
+        cases[name] = _aa_case(x[np.newaxis, :], 512, res)
+
+    # (3) run_single_test-shaped inputs (sync_aa.py:669-740): channel + CFO + 12-bit ADC, 2 RX
+    grid = [(1024, None, 10.0, 1.0), (1024, "cir1", 0.0, 0.5), (512, "cir2", 5.0, 2.0),
+            (256, "cir1", 0.0, 1.0)]
+    for plen, ch, snr, fsr in grid:
+        rng = np.random.default_rng(42)
+        L = plen // 2
+        pre = sa.build_aa_preamble(plen)[0]
+        pil, _ = sa.build_random_qpsk_symbol(rng)
+        dat, _ = sa.build_random_qpsk_symbol(rng)
+        txg = np.concatenate([np.zeros(500, complex), pre, pil, dat, np.zeros(500, complex)])
+        rx, _, _ = sa.apply_channel_multi_antenna(txg, snr, rng, ch, num_rx_antennas=2)
+        rx = sa.apply_cfo(rx, 500.0, sa.SAMPLE_RATE_HZ)
+        fs = np.sqrt(np.mean(np.abs(rx) ** 2)) * fsr
+        rxq = np.stack([sa.quantize_adc(rx[a], fs) for a in range(2)])
+        res = sa.aa_detect_streaming(rxq, L=L)
+        cases[f"aa_grid_len{plen}_{ch or 'awgn'}_snr{int(snr)}_fs{fsr}"] = _aa_case(rxq, L, res)
+
+    # (4) integer (int12) inputs, L=128 (BASELINE cfg2 shape): float64 reference on integer values
+    rng = np.random.default_rng(7)
+    pre = sa.build_aa_preamble(256)[0]
+    pil, _ = sa.build_random_qpsk_symbol(rng)
+    txg = np.concatenate([np.zeros(300, complex), pre, pil, np.zeros(200, complex)])
+    rx, _, _ = sa.apply_channel_multi_antenna(txg, 10.0, rng, "cir1", num_rx_antennas=2)
+    rx = rx[:, :1024]
+    scale = 2046.0 / np.max(np.abs(np.concatenate([rx.real.ravel(), rx.imag.ravel()])))
+    xi = np.clip(np.round(rx.real * scale), -2048, 2047) + 1j * np.clip(np.round(rx.imag * scale), -2048, 2047)
+    res = sa.aa_detect_streaming(xi, L=128)
+    cases["aa_int12_L128"] = _aa_case(xi, 128, res)
+
+    # (5) edge lengths: T < L, T == L, T == 2L-1, T == 2L, tiny L; random data, 1 and 3 antennas
+    rng = np.random.default_rng(11)
+    for T, L, na in ((5, 8, 1), (8, 8, 1), (15, 8, 2), (16, 8, 3), (40, 1, 1), (33, 2, 2)):
+        x = rng.standard_normal((na, T)) + 1j * rng.standard_normal((na, T))
+        res = sa.aa_detect_streaming(x, L=L, threshold=0.1, hysteresis=3)
+        c = _aa_case(x, L, res)
+        c["threshold"] = np.float64(0.1)
+        c["hysteresis"] = np.int64(3)
+        cases[f"aa_edge_T{T}_L{L}_a{na}"] = c
+
+
+def _aa_case(x, L, res):
+    ints, reals = _events_aa(res)
+    st = res.state
+    return dict(kind="aa", x=np.asarray(x, np.complex128), L=np.int64(L), P=st.P, R=st.R, M=st.M,
+                valid=st.valid, ev_int=ints, ev_real=reals,
+                threshold=np.float64(0.15), hysteresis=np.int64(128), sample_rate=np.float64(15.36e6))
+
+
+def gen_sc(R, cases):
+    sc = R["sc"]
+    core = R["core"]
+    ch = R["channel"]
+    # cfg1: N=64, CP=16, SNR=20 dB, one AWGN burst.  build_sc_preamble is hard-wired to 1200
+    # tones (core.py:7), so the N=64 burst is built here: BPSK on even bins within +-30.
+    rng = np.random.default_rng(2026)
+    N, CP = 64, 16
+    idx = np.arange(-30, 31)
+    idx = idx[(idx % 2 == 0) & (idx != 0)]
+    spec = np.zeros(N, complex)
+    spec[(N // 2 + idx) % N] = rng.choice([-1.0, 1.0], size=idx.size)
+    sym = np.fft.ifft(np.fft.ifftshift(spec))
+    sym /= np.sqrt(np.mean(np.abs(sym) ** 2))
+    burst = np.concatenate([np.zeros(100, complex), sym[-CP:], sym, np.zeros(100, complex)])
+    rx = ch.apply_channel(burst, 20.0, rng)
+    _sc_run(sc, rx, 64, "sc_N64_cfg1", cases)
+
+    # N=1024 and N=2048 on sc.run_simulation-shaped streams (sc.py:159-205), truncated
+    rng = np.random.default_rng(0)
+    pre = sc.build_sc_preamble(rng, include_cp=True)      # N_FFT=2048 preamble
+    pil, _ = core.build_random_qpsk_symbol(rng, include_cp=True)
+    tx = np.concatenate([np.zeros(1337, complex), pre, pil])
+    cir = ch.load_measured_cir("cir1")[1:2]
+    rx = core.apply_cfo(ch.apply_channel(tx, 10.0, rng, cir), 1000.0, core.SAMPLE_RATE_HZ)
+    _sc_run(sc, rx[:, :7000], 2048, "sc_N2048_cir1", cases)
+    rx2 = ch.apply_channel(tx[:5000], 5.0, np.random.default_rng(5), ch.load_measured_cir("cir2"))
+    _sc_run(sc, rx2, 1024, "sc_N1024_cir2_2br", cases)
+    # degenerate: T < N (empty outputs) and T == N (one output)
+    _sc_run(sc, rx2[:, :100], 128, "sc_short_empty", cases)
+    _sc_run(sc, rx2[:, :128], 128, "sc_exact_one", cases)
+
+
+def _sc_run(sc, rx, N, name, cases):
+    old = sc.N_FFT
+    sc.N_FFT = N
+    try:
+        M, P, Rr = sc.sc_streaming_metric(rx)
+    finally:
+        sc.N_FFT = old
+    cases[name] = dict(kind="sc", x=np.atleast_2d(np.asarray(rx, np.complex128)), N=np.int64(N),
+                       M=M, P=P, R=Rr)
+
+
+def gen_combined(R, cases):
+    cb = R["combined"]
+    mn = R["minn"]
+    core = R["core"]
+    ch = R["channel"]
+    rng = np.random.default_rng(0)
+    pre = cb.build_minn_preamble(rng, include_cp=True)
+    pil, _ = core.build_random_qpsk_symbol(rng, include_cp=True)
+    tx = np.concatenate([np.zeros(1337, complex), pre, pil])
+    rx = core.apply_cfo(ch.apply_channel(tx, 10.0, rng, ch.load_measured_cir("cir1")[:2]),
+                        1000.0, core.SAMPLE_RATE_HZ)[:, :6500]
+    M, P, Rr = cb.schmidl_cox_streaming_metric(rx)
+    cases["comb_sc_N2048_cir1_2br"] = dict(kind="comb_sc", x=rx, N=np.int64(2048), M=M, P=P, R=Rr)
+    M, P, Rr = cb.schmidl_cox_streaming_metric(rx[:, :3000], symbol_len=256)
+    cases["comb_sc_N256"] = dict(kind="comb_sc", x=rx[:, :3000], N=np.int64(256), M=M, P=P, R=Rr)
+    M, P, Rr = cb.minn_streaming_metric(rx)
+    cases["comb_minn_N2048_cir1_2br"] = dict(kind="minn", x=rx, N=np.int64(2048), M=M, P=P, R=Rr)
+    for N in (256, 258, 512):
+        M, P, Rr = mn.minn_streaming_metric_parameterized(rx[0, :3000], N)
+        cases[f"minn_param_N{N}"] = dict(kind="minn", x=rx[:1, :3000], N=np.int64(N), M=M, P=P, R=Rr)
+
+
+def _rtl_case(R, x, Q, shift, thr, frac, hyst, toff):
+    mr = R["minn_rtl"]
+    st = mr.minn_rtl_streaming_metric(x, smooth_shift=shift, threshold_value=thr,
+                                      threshold_frac_bits=frac, quarter_len=Q)
+    det = mr.detect_minn_rtl(st, hysteresis=hyst, timing_offset=toff)
+    ev = np.array([[e.peak_index, e.detected_index, e.gate_segment[0], e.gate_segment[1]]
+                   for e in det.events], dtype=np.int64).reshape(-1, 4)
+    seg = np.array(det.gate_segments, dtype=np.int64).reshape(-1, 2)
+    return dict(kind="minn_rtl", x=np.atleast_2d(np.asarray(x, np.complex128)), Q=np.int64(Q),
+                smooth_shift=np.int64(shift), threshold_value=np.int64(thr),
+                threshold_frac_bits=np.int64(frac), hysteresis=np.int64(hyst),
+                timing_offset=np.int64(toff),
+                corr_total=st.corr_total, corr_positive=st.corr_positive,
+                smooth_metric=st.smooth_metric, energy_total=st.energy_total,
+                corr_scaled=st.corr_scaled, energy_scaled=st.energy_scaled,
+                metric_valid=st.metric_valid, above_threshold=st.above_threshold,
+                events=ev, gate_segments=seg, gate_mask=det.gate_mask)
+
+
+def gen_minn_rtl(R, cases):
+    mr = R["minn_rtl"]
+    core = R["core"]
+    ch = R["channel"]
+    thr = int(0.10 * (1 << 15))
+    for Q, T, seed in ((64, 1024, 3), (512, 6000, 4)):
+        rng = np.random.default_rng(seed)
+        pre = mr.build_minn_preamble_generic("qpsk_freq", rng, Q=Q)
+        pil, _ = core.build_random_qpsk_symbol(rng, include_cp=True)
+        tx = np.concatenate([np.zeros(3 * Q, complex), pre, pil])
+        rx = ch.apply_channel(tx, 10.0, rng, ch.load_measured_cir("cir1")[:2])[:, :T]
+        # 12-bit quantisation in the style of ref/test_minn_preamble_detector.py:150-161
+        s = 2046.0 / np.max(np.abs(np.concatenate([rx.real.ravel(), rx.imag.ravel()])))
+        xi = np.clip(np.round(rx.real * s), -2048, 2047) + 1j * np.clip(np.round(rx.imag * s), -2048, 2047)
+        cases[f"rtl_Q{Q}_int12"] = _rtl_case(R, xi, Q, 3, thr, 15, 2, 0)
+        if Q == 64:
+            cases["rtl_Q64_float"] = _rtl_case(R, rx, Q, 3, thr, 15, 2, 0)
+            cases["rtl_Q64_int12_noshift_h0"] = _rtl_case(R, xi, Q, 0, thr, 15, 0, -5)
+            cases["rtl_Q64_int12_thr0_h5"] = _rtl_case(R, xi[:1], Q, 2, 0, 15, 5, 7)
+
+
+def gen_cp_cfo(R, cases):
+    core = R["core"]
+    ch = R["channel"]
+    rng = np.random.default_rng(9)
+    sym, _ = core.build_random_qpsk_symbol(rng, include_cp=True)
+    tx = np.concatenate([np.zeros(200, complex), sym, sym])
+    rx = core.apply_cfo(ch.apply_channel(tx, 15.0, rng, ch.load_measured_cir("cir1")[:2]),
+                        1234.5, core.SAMPLE_RATE_HZ)
+    starts = np.array([0, 200, 250, 333, 1000], dtype=np.int64)
+    cfo = np.array([core.estimate_cfo_from_cp(rx, int(s), 2048, 512, core.SAMPLE_RATE_HZ)
+                    for s in starts])
+    cfo1 = np.array([core.estimate_cfo_from_cp(rx[0], int(s), 2048, 256, 15.36e6) for s in starts])
+    cases["cp_cfo"] = dict(kind="cp_cfo", x=rx, starts=starts, n_fft=np.int64(2048),
+                           cp_len=np.int64(512), fs=np.float64(core.SAMPLE_RATE_HZ), cfo=cfo,
+                           cfo_1br_cp256=cfo1, fs_1br=np.float64(15.36e6))
+
+
+def main():
+    R = _import_reference()
+    cases: dict[str, dict] = {}
+    gen_aa(R, cases)
+    gen_sc(R, cases)
+    gen_combined(R, cases)
+    gen_minn_rtl(R, cases)
+    gen_cp_cfo(R, cases)
+    OUT.mkdir(parents=True, exist_ok=True)
+    for name, d in cases.items():
+        arrs = {k: (np.asarray(v) if not isinstance(v, str) else np.array(v)) for k, v in d.items()}
+        np.savez_compressed(OUT / f"{name}.npz", **arrs)
+    (OUT / "MANIFEST.txt").write_text(
+        "Generated by tests/golden/make_golden.py from amcolex/ofdm-sync-math @ /root/reference\n"
+        f"numpy {np.__version__}\n" + "\n".join(sorted(cases)) + "\n")
+    print(f"wrote {len(cases)} cases to {OUT}")
+
+
+if __name__ == "__main__":
+    main()
