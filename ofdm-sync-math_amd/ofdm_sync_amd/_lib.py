@@ -1,0 +1,178 @@
+"""ctypes binding of libofdmsync.so (the C ABI declared in include/ofdmsync.h).
+
+PyTorch is used only as plumbing: device memory, the current HIP stream, host<->device
+copies.  Every metric is computed by the HIP kernels in ``csrc/ofdmsync.hip``.  There is
+no CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_int32, c_int64, c_void_p
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libofdmsync.so")
+
+# input formats / precisions / status (include/ofdmsync.h)
+C64, C128, CI16 = 0, 1, 2
+FP32, FP64 = 0, 1
+
+_lib = None
+
+
+def _declare(lib):
+    P = c_void_p
+    sig = {
+        "ofs_version": (c_int32, []),
+        "ofs_status_string": (ctypes.c_char_p, [c_int32]),
+        "ofs_aa_detect": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P, P,
+                                    P, c_int32, c_double, c_int32, c_double, c_int32, P, P, P, P]),
+        "ofs_sc_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
+                                    c_int32, P, P, P, P]),
+        "ofs_minn_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
+                                      P, P, P, P]),
+        "ofs_minn_rtl": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, c_int32,
+                                   c_int64, c_int32, P, P, P, P, P, P, P, P, c_int32, c_int32,
+                                   c_int32, c_int32, P, P, P, P]),
+        "ofs_minn_rtl_gate": (c_int32, [P, P, P, c_int64, c_int64, c_int32, c_int32, c_int32, P, P,
+                                        P, P]),
+        "ofs_cp_cfo": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_int32,
+                                 c_double, P, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Load libofdmsync.so (after torch, so both share torch's HIP runtime)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "from the repository root (hipcc --offload-arch=gfx950)")
+        l = ctypes.CDLL(LIB_PATH)
+        _declare(l)
+        _lib = l
+    return _lib
+
+
+def require_gpu() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("ofdm_sync_amd needs a ROCm GPU (MI355X / gfx950); no CPU fallback exists")
+    lib()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ofs_status_string(rc).decode()
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        raise RuntimeError(f"{what}: {msg} (status {rc})")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------------------------------
+# input normalisation
+# ------------------------------------------------------------------------------------------
+class Batch:
+    """A device tensor of samples laid out [B][n_branch][T] plus its ABI format code."""
+
+    def __init__(self, data: torch.Tensor, fmt: int, B: int, nb: int, T: int, from_numpy: bool,
+                 exact_default: bool):
+        self.data, self.fmt, self.B, self.nb, self.T = data, fmt, B, nb, T
+        self.from_numpy = from_numpy
+        self.exact_default = exact_default
+
+
+def as_batch(x, batched: bool, *, complex_cast: bool = False) -> Batch:
+    """Normalise reference-style inputs.
+
+    Unbatched (drop-in) semantics follow the reference: 1-D -> one branch, 2-D -> branches on
+    axis 0 (summed).  Batched inputs are [B, n_branch, T] (2-D means [B, T]).  ``int16``
+    inputs carry I/Q in a trailing axis of size 2 (OFS_CI16).  ``complex_cast`` forces
+    complex128 (minn_rtl.py:680 casts to complex128).
+    """
+    dev = require_gpu()
+    from_numpy = not isinstance(x, torch.Tensor)
+    if from_numpy:
+        a = np.asarray(x)
+        if a.dtype == np.int16 and a.ndim >= 1 and a.shape[-1] == 2:
+            t = torch.from_numpy(np.ascontiguousarray(a))
+        else:
+            if complex_cast or not np.iscomplexobj(a) or a.dtype not in (np.complex64, np.complex128):
+                a = a.astype(np.complex128)
+            t = torch.from_numpy(np.ascontiguousarray(a))
+        t = t.to(dev, non_blocking=False)
+    else:
+        t = x
+        if t.device.type != "cuda":
+            t = t.to(dev)
+        if complex_cast and t.dtype != torch.complex128 and t.dtype != torch.int16:
+            t = t.to(torch.complex128)
+        if not (t.is_complex() or (t.dtype == torch.int16 and t.shape[-1] == 2)):
+            t = t.to(torch.complex128)
+    if t.dtype == torch.int16:
+        fmt = CI16
+        core_shape = tuple(t.shape[:-1])
+    elif t.dtype == torch.complex64:
+        fmt = C64
+        core_shape = tuple(t.shape)
+    elif t.dtype == torch.complex128:
+        fmt = C128
+        core_shape = tuple(t.shape)
+    else:
+        raise TypeError(f"unsupported sample dtype {t.dtype}")
+    if batched:
+        if len(core_shape) == 2:
+            B, nb, T = core_shape[0], 1, core_shape[1]
+        elif len(core_shape) == 3:
+            B, nb, T = core_shape
+        else:
+            raise ValueError("batched input must be [B, T] or [B, n_branch, T]")
+    else:
+        if len(core_shape) == 1:
+            B, nb, T = 1, 1, core_shape[0]
+        elif len(core_shape) == 2:
+            B, nb, T = 1, core_shape[0], core_shape[1]
+        else:
+            raise ValueError("input must be 1-D (T,) or 2-D (branches, T)")
+    t = t.contiguous()
+    exact_default = fmt in (C128, CI16)
+    return Batch(t, fmt, B, nb, T, from_numpy, exact_default)
+
+
+def resolve_precision(batch: Batch, precision) -> int:
+    if precision is None:
+        return FP64 if batch.exact_default else FP32
+    if precision in ("fp64", "float64", FP64):
+        return FP64
+    if precision in ("fp32", "float32", FP32):
+        return FP32
+    raise ValueError(f"precision must be None, 'fp32' or 'fp64', got {precision!r}")
+
+
+def out_real(shape, prec: int, dev) -> torch.Tensor:
+    return torch.empty(shape, dtype=torch.float64 if prec == FP64 else torch.float32, device=dev)
+
+
+def out_cplx(shape, prec: int, dev) -> torch.Tensor:
+    return torch.empty(shape, dtype=torch.complex128 if prec == FP64 else torch.complex64, device=dev)
+
+
+def to_host(t: torch.Tensor, dtype=None) -> np.ndarray:
+    a = t.detach().cpu().numpy()
+    return a if dtype is None else a.astype(dtype, copy=False)

@@ -1,0 +1,168 @@
+"""Drop-in for the [A][A] streaming detector of ``sync_aa.py`` (reference: sync_aa.py:421-571).
+
+``aa_detect_streaming`` keeps the reference signature, defaults, dataclasses and field
+names; the P/R/M streams and the gate/peak/CFO events are computed by one fused HIP kernel
+(``ofs_aa_detect``).  ``aa_detect_streaming_batched`` is the native fast path: a batch of
+independent receive streams [B, n_ant, T], device-resident in and out.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+# System constants (sync_aa.py:99-125)
+N_FFT = 1024
+NUM_ACTIVE_SUBCARRIERS = 600
+CYCLIC_PREFIX = 72
+SAMPLE_RATE_HZ = 15_360_000.0
+PREAMBLE_LENGTHS = [1024, 512, 256]
+DEFAULT_PREAMBLE_LEN = 1024
+PREAMBLE_HALF_LEN = DEFAULT_PREAMBLE_LEN // 2
+PREAMBLE_TOTAL_LEN = DEFAULT_PREAMBLE_LEN
+DETECT_THRESHOLD = 0.15
+DETECT_HYSTERESIS = 128
+ADC_BITS = 12
+ADC_LEVELS = 2 ** (ADC_BITS - 1)
+TX_PRE_PAD_SAMPLES = 500
+TX_POST_PAD_SAMPLES = 500
+
+
+@dataclass
+class AADetectorState:
+    """State arrays from streaming detection (sync_aa.py:392-398)."""
+    P: np.ndarray
+    R: np.ndarray
+    M: np.ndarray
+    valid: np.ndarray
+
+
+@dataclass
+class AADetectionEvent:
+    """A single detection event (sync_aa.py:401-410)."""
+    peak_index: int
+    P_at_peak: complex
+    M_at_peak: float
+    gate_start: int
+    gate_end: int
+    cfo_hz: float
+    frame_start: int
+
+
+@dataclass
+class AADetectionResult:
+    """Complete detection result (sync_aa.py:413-418)."""
+    events: list[AADetectionEvent]
+    state: AADetectorState
+    num_antennas: int
+
+
+@dataclass
+class AABatchResult:
+    """Device-resident result of ``aa_detect_streaming_batched``.
+
+    P [B,T] complex, R/M [B,T] real, valid [B,T] bool (None when not requested);
+    n_events [B] int32; ev_int [B,E,4] int64 = (peak_index, gate_start, gate_end, frame_start);
+    ev_real [B,E,4] f64 = (P_re, P_im, M_at_peak, cfo_hz); E = max_events.
+    """
+    P: torch.Tensor | None
+    R: torch.Tensor | None
+    M: torch.Tensor | None
+    valid: torch.Tensor | None
+    n_events: torch.Tensor | None
+    ev_int: torch.Tensor | None
+    ev_real: torch.Tensor | None
+
+
+def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_rate: float,
+         prec: int, want=("P", "R", "M", "valid"), detect: bool = True, max_events: int = 16):
+    dev = batch.data.device
+    B, T = batch.B, batch.T
+    P = _lib.out_cplx((B, T), prec, dev) if "P" in want else None
+    R = _lib.out_real((B, T), prec, dev) if "R" in want else None
+    M = _lib.out_real((B, T), prec, dev) if "M" in want else None
+    V = torch.empty((B, T), dtype=torch.bool, device=dev) if "valid" in want else None
+    n_ev = ev_i = ev_r = None
+    if detect:
+        n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
+        ev_i = torch.empty((B, max(max_events, 1), 4), dtype=torch.int64, device=dev)
+        ev_r = torch.empty((B, max(max_events, 1), 4), dtype=torch.float64, device=dev)
+    rc = _lib.lib().ofs_aa_detect(batch.fmt, batch.data.data_ptr(), B, batch.nb, T, int(L), prec,
+                                  _lib.ptr(P), _lib.ptr(R), _lib.ptr(M), _lib.ptr(V), int(detect),
+                                  float(threshold), int(hysteresis), float(sample_rate),
+                                  int(max_events), _lib.ptr(n_ev), _lib.ptr(ev_i), _lib.ptr(ev_r),
+                                  _lib.stream_ptr())
+    _lib.check(rc, "ofs_aa_detect")
+    return AABatchResult(P, R, M, V, n_ev, ev_i, ev_r)
+
+
+def aa_detect_streaming_batched(x, L: int = PREAMBLE_HALF_LEN, threshold: float = DETECT_THRESHOLD,
+                                hysteresis: int = DETECT_HYSTERESIS,
+                                sample_rate: float = SAMPLE_RATE_HZ, *, precision=None,
+                                outputs=("P", "R", "M", "valid"), detect: bool = True,
+                                max_events: int = 16) -> AABatchResult:
+    """Batched [A][A] detector over independent streams x[B, n_ant, T] (or [B, T]).
+
+    Same per-stream semantics as ``aa_detect_streaming``; results stay on the GPU.
+    ``precision``: None (fp64 for complex128/int16 input, fp32 for complex64), 'fp32', 'fp64'.
+    """
+    batch = _lib.as_batch(x, batched=True)
+    prec = _lib.resolve_precision(batch, precision)
+    want = tuple(outputs)
+    if detect and batch.T > 0:
+        want = tuple(sorted(set(want) | {"P", "M"}, key=["P", "R", "M", "valid"].index))
+    res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, max_events)
+    if detect and batch.B > 0 and batch.T > 0:
+        worst = int(res.n_events.max().item())
+        if worst > max_events:
+            res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, worst)
+    for name in ("P", "R", "M", "valid"):
+        if name not in outputs:
+            setattr(res, name, None)
+    return res
+
+
+def aa_detect_streaming(
+    rx_samples: np.ndarray,
+    L: int = PREAMBLE_HALF_LEN,
+    threshold: float = DETECT_THRESHOLD,
+    hysteresis: int = DETECT_HYSTERESIS,
+    sample_rate: float = SAMPLE_RATE_HZ,
+    *,
+    precision=None,
+) -> AADetectionResult:
+    """Streaming [A][A] detector with multi-antenna support (drop-in for sync_aa.py:421-571).
+
+    rx_samples: (num_antennas, num_samples) or (num_samples,).  Returns AADetectionResult
+    with numpy state arrays (torch input -> torch device tensors).
+    """
+    batch = _lib.as_batch(rx_samples, batched=False)
+    prec = _lib.resolve_precision(batch, precision)
+    num_antennas = batch.nb
+    T = batch.T
+    if T == 0:
+        empty = AADetectorState(P=np.zeros(0, np.complex128), R=np.zeros(0), M=np.zeros(0),
+                                valid=np.zeros(0, bool))
+        return AADetectionResult(events=[], state=empty, num_antennas=num_antennas)
+    max_ev = 16
+    res = _run(batch, L, threshold, hysteresis, sample_rate, prec, detect=True, max_events=max_ev)
+    n = int(res.n_events[0].item())
+    if n > max_ev:
+        res = _run(batch, L, threshold, hysteresis, sample_rate, prec, detect=True, max_events=n)
+    ev_i = res.ev_int[0, :n].cpu().numpy()
+    ev_r = res.ev_real[0, :n].cpu().numpy()
+    events = [
+        AADetectionEvent(peak_index=int(a[0]), P_at_peak=complex(r[0], r[1]), M_at_peak=float(r[2]),
+                         gate_start=int(a[1]), gate_end=int(a[2]), cfo_hz=float(r[3]),
+                         frame_start=int(a[3]))
+        for a, r in zip(ev_i, ev_r)
+    ]
+    if batch.from_numpy:
+        state = AADetectorState(P=_lib.to_host(res.P[0], np.complex128), R=_lib.to_host(res.R[0], np.float64),
+                                M=_lib.to_host(res.M[0], np.float64), valid=_lib.to_host(res.valid[0]))
+    else:
+        state = AADetectorState(P=res.P[0], R=res.R[0], M=res.M[0], valid=res.valid[0])
+    return AADetectionResult(events=events, state=state, num_antennas=num_antennas)

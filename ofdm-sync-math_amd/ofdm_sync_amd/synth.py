@@ -1,0 +1,82 @@
+"""Synthetic receive-stream batches for benchmarks and tests (input synthesis, not the hot path).
+
+Restates the reference's input builders closely enough to produce realistic streams:
+  aa_preamble      <- sync_aa.build_aa_preamble (sync_aa.py:160-235)
+  load_cir         <- channel.load_measured_cir (channel.py:15-48)
+  make_aa_batch    <- run_single_test's channel + AWGN + CFO chain (sync_aa.py:577-645),
+                      vectorised over a batch on the GPU (torch ops; RNG parity with numpy is
+                      not a goal, only the distribution: SURVEY.md §8f row 2).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CIR_DIR = os.path.join(_HERE, "channel_models")
+
+
+def aa_preamble(total_length: int = 1024, n_fft: int = 1024, num_active: int = 600) -> np.ndarray:
+    """[A][A] Zadoff-Chu preamble on every K-th bin (sync_aa.py:160-235)."""
+    K = 2 * n_fft // total_length
+    dc = n_fft // 2
+    half_active = num_active // 2
+    used = np.array([dc + o for o in range(-half_active, half_active + 1) if o != 0 and (dc + o) % K == 0])
+    num_sc = len(used)
+    root = 25 if num_sc % 25 != 0 else 23
+    n = np.arange(num_sc)
+    zc = np.exp(-1j * np.pi * root * n * (n + 1) / num_sc)
+    spec = np.zeros(n_fft, complex)
+    spec[used] = zc
+    full = np.fft.ifft(spec) * np.sqrt(n_fft)
+    pre = full[:total_length]
+    return pre / np.sqrt(np.mean(np.abs(pre) ** 2))
+
+
+def load_cir(name: str = "cir1") -> np.ndarray:
+    """All RX-branch CIRs of a measured profile, [n_branch, taps] complex128."""
+    data = np.genfromtxt(os.path.join(CIR_DIR, f"{name}.csv"), delimiter=",", skip_header=1)
+    if data.ndim == 1:
+        data = data[np.newaxis, :]
+    chans = []
+    for c in range((data.shape[1] - 1) // 2):
+        re, im = data[:, 1 + 2 * c], data[:, 2 + 2 * c]
+        m = np.isfinite(re) & np.isfinite(im)
+        chans.append(re[m] + 1j * im[m])
+    out = np.zeros((len(chans), max(len(c) for c in chans)), complex)
+    for i, c in enumerate(chans):
+        out[i, :len(c)] = c
+    return out
+
+
+def make_aa_batch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, cir: str | None = "cir1",
+                  branch: int = 1, snr_db=(0.0, 15.0), cfo_hz=(-5000.0, 5000.0), fs: float = 15.36e6,
+                  max_offset: int = 128, device="cuda", dtype=torch.complex64) -> torch.Tensor:
+    """Batch [B, 1, T] of received [A][A] preambles: CIR (one branch) + AWGN + CFO, unit power.
+
+    Each stream is a T-sample window of the faded preamble starting at a random offset in
+    [0, max_offset); SNR and CFO are drawn uniformly per stream.
+    """
+    rng = np.random.default_rng(seed)
+    pre = aa_preamble(2 * L)
+    y0 = pre if cir is None else np.convolve(pre, load_cir(cir)[branch])
+    y0 = y0 / np.sqrt(np.mean(np.abs(y0[: 2 * L]) ** 2))
+    pad = np.zeros(T + max_offset, complex)
+    pad[: min(len(y0), len(pad))] = y0[: len(pad)]
+    dev = torch.device(device)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    base = torch.from_numpy(pad).to(dev)
+    off = torch.from_numpy(rng.integers(0, max_offset, B)).to(dev)
+    idx = off[:, None] + torch.arange(T, device=dev)[None, :]
+    sig = base[idx]                                                        # [B, T] c128
+    snr = torch.from_numpy(rng.uniform(*snr_db, B)).to(dev)
+    f = torch.from_numpy(rng.uniform(*cfo_hz, B)).to(dev)
+    nstd = torch.sqrt(10 ** (-snr / 10) / 2)[:, None]
+    noise = torch.complex(torch.randn((B, T), generator=g, device=dev, dtype=torch.float64),
+                          torch.randn((B, T), generator=g, device=dev, dtype=torch.float64)) * nstd
+    n = torch.arange(T, device=dev, dtype=torch.float64)
+    tone = torch.polar(torch.ones((B, T), device=dev, dtype=torch.float64), 2 * np.pi * f[:, None] * n[None, :] / fs)
+    x = (sig * tone + noise).to(dtype)
+    return x[:, None, :].contiguous()

@@ -1,0 +1,89 @@
+"""CPU: the C-ABI library loads, exports every symbol declared in include/ofdmsync.h, and
+rejects bad arguments before touching the GPU.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "ofdmsync.h")
+LIB = os.path.join(ROOT, "ofdm-sync-math_amd", "ofdm_sync_amd", "libofdmsync.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        import __graft_entry__ as g
+        g.build_hip()
+    return ctypes.CDLL(LIB)
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(ofs_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    assert {"ofs_aa_detect", "ofs_sc_metric", "ofs_minn_metric", "ofs_minn_rtl",
+            "ofs_minn_rtl_gate", "ofs_cp_cfo", "ofs_version", "ofs_status_string"} <= set(syms)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+
+
+def test_exports_are_c_linkage():
+    out = os.popen(f"nm -D --defined-only {LIB}").read()
+    exported = set(re.findall(r"\bT\s+(ofs_\w+)$", out, re.M))
+    assert set(declared_symbols()) <= exported
+
+
+def test_version_and_status(lib):
+    lib.ofs_version.restype = ctypes.c_int32
+    assert lib.ofs_version() >= 100
+    lib.ofs_status_string.restype = ctypes.c_char_p
+    lib.ofs_status_string.argtypes = [ctypes.c_int32]
+    assert lib.ofs_status_string(0) == b"ok"
+    assert b"invalid" in lib.ofs_status_string(-1)
+
+
+def test_argument_validation_without_gpu(lib):
+    """Bad arguments return OFS_EINVAL (-1) before any HIP call."""
+    from ofdm_sync_amd import _lib as L
+    L._declare(lib)
+    # null input
+    assert lib.ofs_aa_detect(0, None, 1, 1, 16, 4, 0, None, None, None, None, 0, 0.1, 1, 1.0, 0,
+                             None, None, None, None) == -1
+    # bad format / precision
+    assert lib.ofs_aa_detect(7, 1, 1, 1, 16, 4, 0, None, None, None, None, 0, 0.1, 1, 1.0, 0,
+                             None, None, None, None) == -1
+    assert lib.ofs_sc_metric(0, 1, 1, 1, 16, 8, 0, 9, None, None, None, None) == -1
+    # odd S&C symbol length
+    assert lib.ofs_sc_metric(0, 1, 1, 1, 16, 7, 0, 0, None, None, None, None) == -1
+    # detect requested without event buffers
+    assert lib.ofs_aa_detect(0, 1, 1, 1, 16, 4, 0, None, None, None, None, 1, 0.1, 1, 1.0, 4,
+                             None, None, None, None) == -1
+    # minn_rtl without required outputs / bad Q
+    assert lib.ofs_minn_rtl(0, 1, 1, 1, 16, 4, 3, 0, 3276, 15, None, None, None, None, None, None,
+                            None, None, 0, 2, 0, 0, None, None, None, None) == -1
+    assert lib.ofs_minn_rtl(0, 1, 1, 1, 16, 0, 3, 0, 3276, 15, 1, None, None, 1, None, None,
+                            None, None, 0, 2, 0, 0, None, None, None, None) == -1
+    assert lib.ofs_cp_cfo(0, 1, 1, 1, 16, None, 8, 4, 1.0, None, None, None) == -1
+    assert lib.ofs_minn_rtl_gate(None, None, None, 1, 16, 2, 0, 1, None, None, None, None) == -1
+    # empty batches are valid no-ops
+    assert lib.ofs_sc_metric(0, 1, 0, 1, 16, 8, 0, 0, None, None, None, None) == 0
+    assert lib.ofs_minn_metric(0, 1, 1, 1, 4, 8, 0, None, None, None, None) == 0
+
+
+def test_product_path_refuses_cpu():
+    """No CPU fallback: the drop-in raises when no GPU is present."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ofdm_sync_amd import sync_aa
+    with pytest.raises(RuntimeError, match="GPU"):
+        sync_aa.aa_detect_streaming([1 + 1j] * 32, L=4)

@@ -1,0 +1,375 @@
+"""GPU parity: every drop-in entry point (through the C ABI of libofdmsync.so) against the
+reference's golden vectors and the CPU oracle.
+
+Tolerances (written here, per north_star):
+  fp64 path (complex128 / int16 input): P, R within 1e-11 relative to the stream maximum,
+      M within 1e-12 absolute, event indices exact; integer (int12) inputs bit-exact where the
+      reference is integer-exact (aa P, every minn_rtl array).
+  fp32 path (complex64 input): M within 1e-6 absolute (north_star), P and R within 1e-5
+      relative to the stream maximum.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover - the -m gpu run is on the GPU box
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from ofdm_sync_amd import sync_aa, sc, minn, minn_rtl, combined_sc_min, core, _lib  # noqa: E402
+from test_oracle_golden import _csv_rows, _fmt_rows, unsign_zero  # noqa: E402
+
+
+def G(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def cases(kind):
+    out = []
+    for p in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
+        if str(np.load(p)["kind"]) == kind:
+            out.append(os.path.basename(p)[:-4])
+    return out
+
+
+def relerr(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.size == 0:
+        return 0.0
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def test_native_library_is_the_one_loaded():
+    L = _lib.lib()
+    assert os.path.samefile(L._name, _lib.LIB_PATH)
+    maps = open("/proc/self/maps").read()
+    assert "libofdmsync.so" in maps
+
+
+# ------------------------------------------------------------------ sync_aa ------------
+@pytest.mark.parametrize("name", cases("aa"))
+def test_aa_fp64_vs_reference_golden(name):
+    d = G(name)
+    r = sync_aa.aa_detect_streaming(d["x"], L=int(d["L"]), threshold=float(d["threshold"]),
+                                    hysteresis=int(d["hysteresis"]), sample_rate=float(d["sample_rate"]))
+    st = r.state
+    assert st.P.dtype == np.complex128 and st.M.dtype == np.float64
+    assert relerr(st.P, d["P"]) < 1e-11
+    assert relerr(st.R, d["R"]) < 1e-11
+    assert np.max(np.abs(st.M - d["M"]), initial=0) < 1e-12
+    assert np.array_equal(st.valid, d["valid"])
+    assert r.num_antennas == d["x"].shape[0]
+    ei = np.array([[e.peak_index, e.gate_start, e.gate_end, e.frame_start] for e in r.events]).reshape(-1, 4)
+    er = np.array([[e.P_at_peak.real, e.P_at_peak.imag, e.M_at_peak, e.cfo_hz] for e in r.events]).reshape(-1, 4)
+    assert np.array_equal(ei, d["ev_int"])
+    assert np.allclose(er, d["ev_real"], rtol=1e-10, atol=1e-8)
+    if "int12" in name:
+        assert np.array_equal(st.P, d["P"])      # exact integer sums
+
+
+@pytest.mark.parametrize("csv,case", [("detector_test_vector.csv", "aa_clean_L512"),
+                                      ("detector_cfo_test_vector.csv", "aa_cfo_L512")])
+def test_aa_reproduces_reference_csv_on_gpu(csv, case):
+    header, rows = _csv_rows(csv)
+    d = G(case)
+    r = sync_aa.aa_detect_streaming(d["x"], L=512)
+    idx = [int(row.split(",")[0]) for row in rows]
+    got = _fmt_rows(r.state.P, r.state.R, r.state.M, header.split(","), idx)
+    assert [unsign_zero(g) for g in got] == [unsign_zero(w) for w in rows]
+    assert r.events[0].peak_index == 1523 and r.events[0].frame_start == 500
+    if "cfo" in csv:
+        assert abs(r.events[0].cfo_hz - 500.0) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["aa_clean_L512", "aa_cfo_L512", "aa_grid_len1024_awgn_snr10_fs1.0",
+                                  "aa_grid_len512_cir2_snr5_fs2.0", "aa_grid_len1024_cir1_snr0_fs0.5"])
+def test_aa_fp32_vs_reference_golden(name):
+    d = G(name)
+    x = torch.from_numpy(d["x"].astype(np.complex64)).cuda()
+    r = sync_aa.aa_detect_streaming(x, L=int(d["L"]))
+    M = r.state.M.cpu().numpy()
+    assert r.state.M.dtype == torch.float32
+    assert np.max(np.abs(M - d["M"])) < 1e-6
+    assert relerr(r.state.P.cpu().numpy(), d["P"]) < 1e-5
+    assert relerr(r.state.R.cpu().numpy(), d["R"]) < 1e-5
+    ref = d["ev_int"]
+    assert len(r.events) == len(ref)
+    for e, (pk, gs, ge, fs_) in zip(r.events, ref):
+        assert abs(e.gate_start - gs) <= 1 and abs(e.gate_end - ge) <= 1
+        assert abs(e.peak_index - pk) <= 2
+    for e, er in zip(r.events, d["ev_real"]):
+        assert abs(e.cfo_hz - er[3]) < 0.5       # Hz
+
+
+def test_aa_int16_iq_input_exact():
+    d = G("aa_int12_L128")
+    x = d["x"]
+    iq = np.stack([x.real, x.imag], axis=-1).astype(np.int16)[None]        # [1, 2, T, 2]
+    out = sync_aa.aa_detect_streaming_batched(torch.from_numpy(iq).cuda(), L=128)
+    assert out.P.dtype == torch.complex128
+    assert np.array_equal(out.P[0].cpu().numpy(), d["P"])
+    Pq, Rq, Mq, _ = O.aa_metric(x, 128)
+    assert np.array_equal(out.R[0].cpu().numpy(), Rq)                         # re²+im² integers
+    assert np.max(np.abs(out.M[0].cpu().numpy() - d["M"])) < 1e-12
+    assert int(out.n_events[0]) == len(d["ev_int"])
+    assert np.array_equal(out.ev_int[0, :len(d["ev_int"])].cpu().numpy(), d["ev_int"])
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+@pytest.mark.parametrize("seed", range(6))
+def test_aa_batched_random_vs_oracle(seed, prec):
+    rng = np.random.default_rng(100 + seed)
+    B = int(rng.integers(1, 40))
+    nb = int(rng.integers(1, 4))
+    T = int(rng.choice([1, 7, 64, 513, 1024, 2048, 3000, 4500, 9000]))
+    L = int(rng.choice([1, 3, 32, 128, 256, 512, 1000]))
+    x = rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))
+    # plant an [A][A] burst in half the streams so gates open
+    for b in range(0, B, 2):
+        if T >= 2 * L + 10:
+            s = int(rng.integers(0, T - 2 * L))
+            a = (rng.standard_normal(L) + 1j * rng.standard_normal(L)) * 3
+            x[b, :, s:s + L] += a
+            x[b, :, s + L:s + 2 * L] += a
+    xt = torch.from_numpy(x if prec == "fp64" else x.astype(np.complex64)).cuda()
+    thr, hyst = 0.2, int(rng.choice([1, 5, 64]))
+    out = sync_aa.aa_detect_streaming_batched(xt, L=L, threshold=thr, hysteresis=hyst, precision=prec)
+    P, R, M = out.P.cpu().numpy(), out.R.cpu().numpy(), out.M.cpu().numpy()
+    nev = out.n_events.cpu().numpy()
+    for b in range(B):
+        xb = x[b] if prec == "fp64" else x[b].astype(np.complex64).astype(np.complex128)
+        Pr, Rr, Mr, vr, ei, er = O.aa_detect(xb, L, thr, hyst)
+        if prec == "fp64":
+            assert relerr(P[b], Pr) < 1e-11 and relerr(R[b], Rr) < 1e-11
+            assert np.max(np.abs(M[b] - Mr), initial=0) < 1e-12
+            assert nev[b] == len(ei)
+            assert np.array_equal(out.ev_int[b, :nev[b]].cpu().numpy(), ei)
+            assert np.allclose(out.ev_real[b, :nev[b]].cpu().numpy(), er, rtol=1e-9, atol=1e-7)
+        else:
+            assert np.max(np.abs(M[b] - Mr), initial=0) < 1e-6
+            assert relerr(P[b], Pr) < 1e-5 and relerr(R[b], Rr) < 1e-5
+        assert np.array_equal(out.valid[b].cpu().numpy(), vr)
+
+
+def test_aa_edge_lengths():
+    r = sync_aa.aa_detect_streaming(np.zeros(0, complex), L=8)
+    assert r.events == [] and r.state.M.size == 0
+    r = sync_aa.aa_detect_streaming(np.ones(5, complex), L=8)
+    assert not r.state.valid.any() and np.all(r.state.M == 0) and r.events == []
+    # constant input: M == 1 everywhere valid, one unclosed gate, first max wins
+    r = sync_aa.aa_detect_streaming(np.ones(64, complex), L=8, threshold=0.5, hysteresis=3)
+    Pr, Rr, Mr, vr, ei, er = O.aa_detect(np.ones(64, complex), 8, 0.5, 3)
+    assert np.array_equal([[e.peak_index, e.gate_start, e.gate_end, e.frame_start] for e in r.events], ei)
+
+
+def test_aa_many_events_grow_buffer():
+    """More events than the initial event buffer: the wrapper re-runs with room for all."""
+    T, L = 6000, 4
+    x = np.zeros(T, complex)
+    for k in range(40):
+        s = 100 + 140 * k
+        x[s:s + 2 * L] = 1.0
+    r = sync_aa.aa_detect_streaming(x, L=L, threshold=0.5, hysteresis=3)
+    Pr, Rr, Mr, vr, ei, er = O.aa_detect(x, L, 0.5, 3)
+    assert len(r.events) == len(ei) > 16
+    assert np.array_equal([[e.peak_index, e.gate_start, e.gate_end, e.frame_start] for e in r.events], ei)
+
+
+# ------------------------------------------------------- sc / combined / minn ------------
+def _window_call(kind, x, N, prec=None):
+    if kind == "sc":
+        old = sc.N_FFT
+        sc.N_FFT = N
+        try:
+            return sc.sc_streaming_metric(x, precision=prec)
+        finally:
+            sc.N_FFT = old
+    if kind == "comb_sc":
+        return combined_sc_min.schmidl_cox_streaming_metric(x, symbol_len=N, precision=prec)
+    return minn.minn_streaming_metric_parameterized(x, N, precision=prec)
+
+
+@pytest.mark.parametrize("name", cases("sc") + cases("comb_sc") + cases("minn"))
+def test_window_metrics_fp64_vs_reference_golden(name):
+    d = G(name)
+    kind = str(d["kind"])
+    M, P, R = _window_call(kind, d["x"], int(d["N"]))
+    assert M.shape == d["M"].shape and P.dtype == np.complex128
+    if M.size:
+        assert relerr(P, d["P"]) < 1e-11
+        assert relerr(R, d["R"]) < 1e-11
+        assert np.max(np.abs(M - d["M"])) < 1e-10
+
+
+@pytest.mark.parametrize("name", ["sc_N64_cfg1", "sc_N2048_cir1", "sc_N1024_cir2_2br",
+                                  "comb_sc_N2048_cir1_2br", "comb_minn_N2048_cir1_2br", "minn_param_N256"])
+def test_window_metrics_fp32_vs_reference_golden(name):
+    d = G(name)
+    kind = str(d["kind"])
+    x = torch.from_numpy(d["x"].astype(np.complex64)).cuda()
+    M, P, R = _window_call(kind, x, int(d["N"]))
+    assert M.dtype == torch.float32
+    assert np.max(np.abs(M.cpu().numpy() - d["M"])) < 1e-6
+    assert relerr(P.cpu().numpy(), d["P"]) < 1e-5
+    assert relerr(R.cpu().numpy(), d["R"]) < 1e-5
+
+
+def test_module_global_n_fft_is_read_at_call_time():
+    d = G("sc_N64_cfg1")
+    sc.N_FFT = 64
+    try:
+        M, P, R = sc.sc_streaming_metric(d["x"])
+    finally:
+        sc.N_FFT = 2048
+    assert np.max(np.abs(M - d["M"])) < 1e-10
+    d = G("comb_minn_N2048_cir1_2br")
+    M, P, R = combined_sc_min.minn_streaming_metric(d["x"])
+    assert np.max(np.abs(M - d["M"])) < 1e-10
+    M, P, R = minn.minn_streaming_metric(d["x"])
+    assert np.max(np.abs(M - d["M"])) < 1e-10
+
+
+def test_window_metric_edges():
+    x = np.ones((2, 100), complex)
+    old = sc.N_FFT
+    sc.N_FFT = 128
+    try:
+        M, P, R = sc.sc_streaming_metric(x)
+        assert M.size == 0 and P.size == 0 and R.size == 0
+        sc.N_FFT = 63
+        with pytest.raises(ValueError):
+            sc.sc_streaming_metric(x)
+    finally:
+        sc.N_FFT = old
+    M, P, R = combined_sc_min.schmidl_cox_streaming_metric(x, symbol_len=1)
+    assert M.size == 0
+    M, P, R = minn.minn_streaming_metric_parameterized(x, 3)   # Q = 0: zero metric
+    Mr, Pr, Rr = O.minn_metric(x, 3)
+    assert np.array_equal(M, Mr) and np.allclose(P, Pr)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_window_metrics_batched_random(seed):
+    rng = np.random.default_rng(7 + seed)
+    B, nb = int(rng.integers(1, 20)), int(rng.integers(1, 3))
+    T = int(rng.choice([300, 2048, 5000, 7000]))
+    N = int(rng.choice([16, 64, 256, 1024, 2048]))
+    x = rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))
+    xt = torch.from_numpy(x).cuda()
+    for kind, fn in (("sc", sc.sc_streaming_metric_batched),
+                     ("comb_sc", combined_sc_min.schmidl_cox_streaming_metric_batched),
+                     ("minn", minn.minn_streaming_metric_batched)):
+        M, P, R = fn(xt, N)
+        ofn = {"sc": O.sc_metric, "comb_sc": O.comb_sc_metric, "minn": O.minn_metric}[kind]
+        for b in range(B):
+            Mr, Pr, Rr = ofn(x[b], N)
+            assert relerr(P[b].cpu().numpy(), Pr) < 1e-11, kind
+            assert np.max(np.abs(M[b].cpu().numpy() - Mr), initial=0) < 1e-10, kind
+
+
+# ---------------------------------------------------------------- minn_rtl ------------
+RTL_KEYS = ("corr_total", "corr_positive", "smooth_metric", "energy_total", "corr_scaled",
+            "energy_scaled", "metric_valid", "above_threshold")
+
+
+@pytest.mark.parametrize("name", cases("minn_rtl"))
+def test_minn_rtl_vs_reference_golden(name):
+    d = G(name)
+    st = minn_rtl.minn_rtl_streaming_metric(
+        d["x"], smooth_shift=int(d["smooth_shift"]), threshold_value=int(d["threshold_value"]),
+        threshold_frac_bits=int(d["threshold_frac_bits"]), quarter_len=int(d["Q"]))
+    exact = "int12" in name
+    for k in RTL_KEYS:
+        got = getattr(st, k)
+        if exact:
+            assert np.array_equal(got, d[k]), k          # bit-exact integer path
+        else:
+            assert np.allclose(got, d[k], rtol=1e-9, atol=1e-6), k
+    det = minn_rtl.detect_minn_rtl(st, hysteresis=int(d["hysteresis"]), timing_offset=int(d["timing_offset"]))
+    ev = np.array([[e.peak_index, e.detected_index, *e.gate_segment] for e in det.events]).reshape(-1, 4)
+    assert np.array_equal(ev, d["events"])
+    assert np.array_equal(np.array(det.gate_segments).reshape(-1, 2), d["gate_segments"])
+    assert np.array_equal(det.gate_mask, d["gate_mask"])
+
+
+@pytest.mark.parametrize("name", ["rtl_Q64_int12", "rtl_Q512_int12", "rtl_Q64_int12_noshift_h0"])
+def test_minn_rtl_batched_int16_fused_gate(name):
+    d = G(name)
+    x = d["x"]
+    iq = np.stack([x.real, x.imag], axis=-1).astype(np.int16)
+    iq = np.stack([iq, iq[:, ::-1].copy()])          # second stream = time-reversed copy
+    out = minn_rtl.minn_rtl_batched(torch.from_numpy(iq).cuda(), int(d["Q"]),
+                                    smooth_shift=int(d["smooth_shift"]), threshold_value=int(d["threshold_value"]),
+                                    threshold_frac_bits=int(d["threshold_frac_bits"]),
+                                    hysteresis=int(d["hysteresis"]), timing_offset=int(d["timing_offset"]))
+    for k in RTL_KEYS:
+        assert np.array_equal(getattr(out, k)[0].cpu().numpy(), d[k]), k
+    n = int(out.n_events[0])
+    assert np.array_equal(out.events[0, :n].cpu().numpy(), d["events"])
+    xr = (iq[1, ..., 0] + 1j * iq[1, ..., 1]).astype(np.complex128)
+    s = O.minn_rtl_metric(xr, int(d["Q"]), int(d["smooth_shift"]), int(d["threshold_value"]), int(d["threshold_frac_bits"]))
+    for k in RTL_KEYS:
+        assert np.array_equal(getattr(out, k)[1].cpu().numpy(), s[k]), k
+    ev, seg, mask = O.detect_minn_rtl(s["corr_positive"], s["above_threshold"], s["metric_valid"],
+                                      int(d["hysteresis"]), int(d["timing_offset"]))
+    n1 = int(out.n_events[1])
+    assert np.array_equal(out.events[1, :n1].cpu().numpy(), ev)
+
+
+def test_minn_rtl_floor_mode_matches_oracle():
+    d = G("rtl_Q64_int12")
+    st = minn_rtl.minn_rtl_streaming_metric(d["x"], smooth_shift=3, threshold_value=3276,
+                                            threshold_frac_bits=15, quarter_len=64, smooth_mode="floor")
+    s = O.minn_rtl_metric(d["x"], 64, 3, 3276, 15, smooth_mode="floor")
+    for k in RTL_KEYS:
+        assert np.array_equal(getattr(st, k), s[k]), k
+
+
+def test_minn_rtl_rejects_bad_quarter():
+    with pytest.raises(ValueError):
+        minn_rtl.minn_rtl_streaming_metric(np.ones(10), smooth_shift=3, threshold_value=1,
+                                           threshold_frac_bits=15, quarter_len=0)
+
+
+# ---------------------------------------------------------------- CP CFO ------------
+def test_cp_cfo_vs_reference_golden():
+    d = G("cp_cfo")
+    got = [core.estimate_cfo_from_cp(d["x"], int(s), int(d["n_fft"]), int(d["cp_len"]), float(d["fs"]))
+           for s in d["starts"]]
+    assert np.allclose(got, d["cfo"], rtol=0, atol=1e-9)
+    got1 = [core.estimate_cfo_from_cp(d["x"][0], int(s), 2048, 256, float(d["fs_1br"])) for s in d["starts"]]
+    assert np.allclose(got1, d["cfo_1br_cp256"], rtol=0, atol=1e-9)
+    xb = torch.from_numpy(np.stack([d["x"]] * len(d["starts"]))).cuda()
+    c = core.estimate_cfo_from_cp_batched(xb, d["starts"], 2048, 512, float(d["fs"]))
+    assert np.allclose(c.cpu().numpy(), d["cfo"], rtol=0, atol=1e-9)
+
+
+# ------------------------------------------------------- full-size (BASELINE cfg3) ------------
+def test_aa_fp32_full_batch_properties():
+    """B = 65536 streams x T = 1024 c64, L = 512: oracle on a sample of streams, invariants
+    on all of them (valid mask, 0 <= M <= 1, scale invariance of M, P/R scale as |a|²)."""
+    B, T, L = 65536, 1024, 512
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    x = torch.randn((B, 1, T), dtype=torch.complex64, device="cuda", generator=g)
+    x[:, :, 512:] += x[:, :, :512].clone()            # [A][A]-like correlation in every stream
+    out = sync_aa.aa_detect_streaming_batched(x, L=L, precision="fp32")
+    M = out.M
+    assert bool((M[:, :L] == 0).all()) and bool((M >= 0).all()) and bool((M <= 1).all())
+    assert bool(out.valid[:, L:].all()) and not bool(out.valid[:, :L].any())
+    idx = torch.randint(0, B, (48,), generator=g, device="cuda").cpu().numpy()
+    xs = x[idx].cpu().numpy().astype(np.complex128)
+    for k, b in enumerate(idx):
+        Pr, Rr, Mr, vr = O.aa_metric(xs[k], L)
+        assert np.max(np.abs(M[b].cpu().numpy() - Mr)) < 1e-6
+    out2 = sync_aa.aa_detect_streaming_batched(x * 2, L=L, precision="fp32")
+    assert torch.max(torch.abs(out2.M - M)).item() < 1e-6
+    assert torch.allclose(out2.R, 4 * out.R, rtol=1e-5)
+    # every stream has its gate open at the end (correlated second half) -> >= 1 event
+    assert bool((out.n_events >= 1).all())

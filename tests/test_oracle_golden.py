@@ -1,0 +1,167 @@
+"""CPU: the oracle against the reference's own fixtures and the captured golden vectors,
+plus a CPU check of the closed-form (parallel) event formulation used by the HIP kernel."""
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+from conftest import GOLDEN
+
+CASES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def _load(path):
+    return np.load(path, allow_pickle=False)
+
+
+def test_fixture_inventory():
+    names = {os.path.basename(p)[:-4] for p in CASES}
+    assert {"aa_clean_L512", "aa_cfo_L512", "aa_int12_L128", "sc_N64_cfg1",
+            "comb_sc_N2048_cir1_2br", "comb_minn_N2048_cir1_2br", "rtl_Q64_int12",
+            "rtl_Q512_int12", "cp_cfo"} <= names
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_matches_reference_golden(path):
+    d = _load(path)
+    kind = str(d["kind"])
+    if kind == "aa":
+        P, R, M, valid, ei, er = O.aa_detect(d["x"], int(d["L"]), float(d["threshold"]),
+                                             int(d["hysteresis"]), float(d["sample_rate"]))
+        scale = max(1.0, float(np.abs(d["P"]).max(initial=0)))
+        assert np.max(np.abs(P - d["P"]), initial=0) <= 1e-12 * scale
+        assert np.max(np.abs(R - d["R"]), initial=0) <= 1e-12 * max(1.0, float(d["R"].max(initial=0)))
+        assert np.max(np.abs(M - d["M"]), initial=0) <= 1e-12
+        assert np.array_equal(valid, d["valid"])
+        assert np.array_equal(ei, d["ev_int"])
+        assert np.allclose(er, d["ev_real"], rtol=1e-12, atol=1e-9)
+        if "int12" in path:
+            # integer inputs: P is an exact integer sum.  R is not: the reference squares
+            # np.abs(x) (a rounded hypot, sync_aa.py:479), so it is only ~1 ulp-exact.
+            assert np.array_equal(P, d["P"])
+            assert np.allclose(R, d["R"], rtol=1e-14, atol=0)
+    elif kind in ("sc", "comb_sc", "minn"):
+        fn = {"sc": O.sc_metric, "comb_sc": O.comb_sc_metric, "minn": O.minn_metric}[kind]
+        M, P, R = fn(d["x"], int(d["N"]))
+        assert M.shape == d["M"].shape
+        if M.size:
+            s = float(np.abs(d["P"]).max())
+            assert np.max(np.abs(P - d["P"])) <= 1e-12 * max(s, 1.0) * 1e3
+            assert np.max(np.abs(R - d["R"])) <= 1e-12 * float(d["R"].max()) * 1e3
+            assert np.max(np.abs(M - d["M"])) <= 1e-10
+    elif kind == "minn_rtl":
+        s = O.minn_rtl_metric(d["x"], int(d["Q"]), int(d["smooth_shift"]), int(d["threshold_value"]),
+                              int(d["threshold_frac_bits"]))
+        exact = "int12" in path
+        for k, v in s.items():
+            if exact:
+                assert np.array_equal(v, d[k]), k
+            else:
+                assert np.allclose(v, d[k], rtol=1e-9, atol=1e-6), k
+        ev, seg, mask = O.detect_minn_rtl(s["corr_positive"], s["above_threshold"], s["metric_valid"],
+                                          int(d["hysteresis"]), int(d["timing_offset"]))
+        assert np.array_equal(ev, d["events"])
+        assert np.array_equal(seg, d["gate_segments"])
+        assert np.array_equal(mask, d["gate_mask"])
+    elif kind == "cp_cfo":
+        c = [O.cp_cfo(d["x"], int(s), int(d["n_fft"]), int(d["cp_len"]), float(d["fs"]))[0] for s in d["starts"]]
+        assert np.allclose(c, d["cfo"], rtol=0, atol=1e-9)
+        c1 = [O.cp_cfo(d["x"][0], int(s), 2048, 256, float(d["fs_1br"]))[0] for s in d["starts"]]
+        assert np.allclose(c1, d["cfo_1br_cp256"], rtol=0, atol=1e-9)
+    else:
+        pytest.fail(kind)
+
+
+def _csv_rows(name):
+    lines = open(os.path.join(GOLDEN, name)).read().splitlines()
+    rows = [ln for ln in lines if ln and not ln.startswith("#")]
+    return rows[0], rows[1:]
+
+
+_NEG_ZERO = re.compile(r"-(0\.0+)(?=,|$)")
+
+
+def unsign_zero(row: str) -> str:
+    """'-0.00' -> '0.00': the sign of a ~1e-17 rounding residue is not part of the value
+    (the reference's recursive sums and a prefix-sum restatement leave residues of either
+    sign where the true P is exactly 0)."""
+    return _NEG_ZERO.sub(r"\1", row)
+
+
+def _fmt_rows(P, R, M, cols, idx):
+    out = []
+    for n in idx:
+        p = P[n]
+        if cols[-1] == "R":
+            out.append("%d,%.8f,%.2f,%.2f,%.2f,%.2f" % (n, M[n], p.real, p.imag, abs(p) ** 2, R[n]))
+        else:
+            out.append("%d,%.8f,%.2f,%.2f,%.2f,%.8f" % (n, M[n], p.real, p.imag, abs(p) ** 2, np.angle(p)))
+    return out
+
+
+@pytest.mark.parametrize("csv,case", [("detector_test_vector.csv", "aa_clean_L512"),
+                                      ("detector_cfo_test_vector.csv", "aa_cfo_L512")])
+def test_oracle_reproduces_reference_csv(csv, case):
+    """docs/detector*_test_vector.csv reproduced string-for-string, up to the
+    sign of printed zeros."""
+    header, rows = _csv_rows(csv)
+    cols = header.split(",")
+    d = _load(os.path.join(GOLDEN, case + ".npz"))
+    P, R, M, _ = O.aa_metric(d["x"], 512)
+    idx = [int(r.split(",")[0]) for r in rows]
+    assert [unsign_zero(r) for r in _fmt_rows(P, R, M, cols, idx)] == [unsign_zero(r) for r in rows]
+
+
+def test_preamble_vector_matches_golden_input():
+    """docs/preamble_test_vector.csv holds the [A][A] preamble that sits at 500..1523 of the
+    detector-vector input; its int12 column is round(x*1024)."""
+    d = _load(os.path.join(GOLDEN, "aa_clean_L512.npz"))
+    tab = np.genfromtxt(os.path.join(GOLDEN, "preamble_test_vector.csv"), delimiter=",", skip_header=1)
+    pre = d["x"][0, 500:1524]
+    assert np.max(np.abs(tab[:, 1] - pre.real)) < 1e-9 and np.max(np.abs(tab[:, 2] - pre.imag)) < 1e-9
+    assert np.array_equal(tab[:, 3], np.round(pre.real * 1024)) and np.array_equal(tab[:, 4], np.round(pre.imag * 1024))
+
+
+# ---------------------------------------------------------------------------------------
+# closed-form gate/peak formulation (what win_kernel/aa_events implements) vs the loop FSM
+# ---------------------------------------------------------------------------------------
+def events_closed_form(P, M, valid, L, thr, hyst, fs):
+    T = len(M)
+    Hp = max(hyst, 1)
+    above = valid & (M >= thr)
+    pos = np.where(above, np.arange(T), -1)
+    prev_incl = np.maximum.accumulate(pos) if T else pos
+    prev_excl = np.concatenate([[-1], prev_incl[:-1]]) if T else pos
+    n = np.arange(T)
+    close = valid & (prev_incl >= 0) & (n - prev_incl == Hp)
+    opn = above & ((prev_excl < 0) | (n - 1 - prev_excl >= Hp))
+    opens, closes = np.flatnonzero(opn), np.flatnonzero(close)
+    pm = np.abs(P) ** 2
+    ints, reals = [], []
+    for k, o in enumerate(opens):
+        c = closes[k] if k < len(closes) else None
+        hi = T - 1 if c is None else c
+        pk = o + int(np.argmax(pm[o:hi + 1]))
+        ints.append((pk, o, T if c is None else c, pk - 2 * L + 1))
+        reals.append((P[pk].real, P[pk].imag, M[pk], np.angle(P[pk]) * fs / (2 * np.pi * L)))
+    return np.array(ints, np.int64).reshape(-1, 4), np.array(reals).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_closed_form_events_equal_loop_fsm(seed):
+    rng = np.random.default_rng(seed)
+    T = int(rng.integers(1, 3000))
+    L = int(rng.integers(1, 300))
+    hyst = int(rng.choice([0, 1, 2, 3, 7, 128]))
+    thr = float(rng.uniform(0.05, 0.9))
+    # bursty metric so gates open/close many times; |P|² with deliberate ties
+    M = np.clip(rng.standard_normal(T).cumsum() * 0.05 + 0.3, 0, 1)
+    P = (rng.integers(0, 5, T) + 1j * rng.integers(0, 3, T)).astype(np.complex128)
+    valid = np.arange(T) >= L
+    ref_i, ref_r = O.aa_events(P, M, valid, L, thr, hyst, 15.36e6)
+    cf_i, cf_r = events_closed_form(P, M, valid, L, thr, hyst, 15.36e6)
+    assert np.array_equal(ref_i, cf_i)
+    assert np.allclose(ref_r, cf_r)
