@@ -172,7 +172,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "win_kernel<C64,fp32,AA> (fused metric + events)",
+                         "kernel": "aa_fast_kernel<NA=1,E=8,MR=1> (wave per stream, fused metric + events)",
                          "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(ms / a.steps, 5)},
             "events_per_stream": round(float(n_ev.float().mean().item()), 3),

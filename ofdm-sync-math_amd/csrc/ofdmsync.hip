@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <math.h>
 #include "ofdmsync.h"
+#include "ofs_common.h"
 
 namespace {
 
@@ -306,11 +307,12 @@ __global__ __launch_bounds__(WG) void win_kernel(WinArgs a) {
         }
         __syncthreads();
         for (int i = tid; i < len; i += WG) {
-            const R re = xs[2 * i], im = xs[2 * i + 1];
-            const R e = re * re + im * im;
-            R pr = 0, pi = 0;
+            // products in fp64 from the stored samples (exact for fp32 / int16 samples)
+            const double re = xs[2 * i], im = xs[2 * i + 1];
+            const double e = re * re + im * im;
+            double pr = 0, pi = 0;
             if (i >= a.D) {
-                const R dr = xs[2 * (i - a.D)], di = xs[2 * (i - a.D) + 1];
+                const double dr = xs[2 * (i - a.D)], di = xs[2 * (i - a.D) + 1];
                 if constexpr (MODE == M_RTL) {
                     pr = dr * re + di * im;          // minn_rtl.py:616
                 } else {
@@ -319,13 +321,13 @@ __global__ __launch_bounds__(WG) void win_kernel(WinArgs a) {
                 }
             }
             if (br == 0) {
-                acc[i] = (double)pr;
-                if constexpr (NQV == 3) acc[LM + i] = (double)pi;
-                acc[(NQV - 1) * LM + i] = (double)e;
+                acc[i] = pr;
+                if constexpr (NQV == 3) acc[LM + i] = pi;
+                acc[(NQV - 1) * LM + i] = e;
             } else {
-                acc[i] += (double)pr;
-                if constexpr (NQV == 3) acc[LM + i] += (double)pi;
-                acc[(NQV - 1) * LM + i] += (double)e;
+                acc[i] += pr;
+                if constexpr (NQV == 3) acc[LM + i] += pi;
+                acc[(NQV - 1) * LM + i] += e;
             }
         }
         __syncthreads();
@@ -413,21 +415,22 @@ __global__ __launch_bounds__(WG) void win_kernel(WinArgs a) {
                 Rr = pref(2, b1) - pref(2, a0);
                 ok = true;
             }
+            // metric in fp64 (sync_aa.py:486-493, sc.py:76-77, minn.py:109-111), stored as R
             const R pr = (R)Pr, pi = (R)Pi, rr = (R)Rr;
-            const R pm = pr * pr + pi * pi;
-            R m;
+            const double pmd = Pr * Pr + Pi * Pi;
+            double md;
             if constexpr (MODE == M_AA) {
-                const R floor_ = (R)(1e-6 * (double)a.W);
-                m = (ok && rr > floor_) ? pm / (rr * rr) : (R)0;
-                m = m < (R)1 ? m : (R)1;
+                md = (ok && Rr > 1e-6 * (double)a.W) ? pmd / (Rr * Rr) : 0.0;
+                md = md < 1.0 ? md : 1.0;
             } else if constexpr (MODE == M_MINN) {
-                const R re_pos = pr > (R)0 ? pr : (R)0;
-                const R den = rr > (R)1e-12 ? rr : (R)1e-12;
-                m = re_pos * re_pos / (den * den);
+                const double re_pos = Pr > 0.0 ? Pr : 0.0;
+                const double den = Rr > 1e-12 ? Rr : 1e-12;
+                md = re_pos * re_pos / (den * den);
             } else {
-                const R den = rr > (R)1e-12 ? rr : (R)1e-12;
-                m = pm / (den * den);
+                const double den = Rr > 1e-12 ? Rr : 1e-12;
+                md = pmd / (den * den);
             }
+            const R m = (R)md, pm = (R)pmd;
             if (a.P) { R* P = reinterpret_cast<R*>(a.P); P[2 * oi] = pr; P[2 * oi + 1] = pi; }
             if (a.R) reinterpret_cast<R*>(a.R)[oi] = rr;
             if (a.M) reinterpret_cast<R*>(a.M)[oi] = m;
@@ -760,6 +763,15 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
         return OFS_EINVAL;
     if (B == 0 || T == 0) return OFS_OK;
     hipStream_t st = (hipStream_t)stream;
+    {   // register-resident fast path (aa_fast.hip) when the shape allows it
+        AaFastArgs f{};
+        f.x = x; f.B = B; f.T = T; f.L = L; f.P = P; f.R = R; f.M = M; f.valid = valid;
+        f.detect = detect; f.thr = threshold; f.hyst = hysteresis; f.fs = sample_rate;
+        f.max_ev = max_events; f.n_ev = n_events; f.ev_i = ev_int; f.ev_r = ev_real;
+        const int frc = ofs_aa_fast_try(in_fmt, precision, n_ant, f, st);
+        if (frc == 1) return OFS_OK;
+        if (frc < 0) return frc;
+    }
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = T; a.nb = n_ant; a.D = L; a.W = L;
     a.P = P; a.R = R; a.M = M; a.valid = valid;

@@ -1,0 +1,89 @@
+// ofs_common.h — device helpers shared by the HIP translation units of libofdmsync.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ofs {
+
+// ---- cross-lane (wave64) helpers: DPP row shifts + row broadcasts (GFX9-family DPP) ----
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = dpp_i<CTRL>(__double2loint(v));
+    const int hi = dpp_i<CTRL>(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+// inclusive wave64 prefix sum of doubles (rocPRIM-style gfx9 DPP ladder)
+__device__ __forceinline__ double wave_scan_add(double v, int lane) {
+    const int rl = lane & 15;
+    double t;
+    t = dpp_d<0x111>(v); if (rl >= 1) v += t;          // row_shr:1
+    t = dpp_d<0x112>(v); if (rl >= 2) v += t;          // row_shr:2
+    t = dpp_d<0x114>(v); if (rl >= 4) v += t;          // row_shr:4
+    t = dpp_d<0x118>(v); if (rl >= 8) v += t;          // row_shr:8
+    t = dpp_d<0x142>(v); if ((lane & 31) >= 16) v += t; // row_bcast:15
+    t = dpp_d<0x143>(v); if (lane >= 32) v += t;        // row_bcast:31
+    return v;
+}
+
+// inclusive wave64 prefix max of ints
+__device__ __forceinline__ int wave_scan_max(int v, int lane) {
+    const int rl = lane & 15;
+    int t;
+    t = dpp_i<0x111>(v); if (rl >= 1) v = max(v, t);
+    t = dpp_i<0x112>(v); if (rl >= 2) v = max(v, t);
+    t = dpp_i<0x114>(v); if (rl >= 4) v = max(v, t);
+    t = dpp_i<0x118>(v); if (rl >= 8) v = max(v, t);
+    t = dpp_i<0x142>(v); if ((lane & 31) >= 16) v = max(v, t);
+    t = dpp_i<0x143>(v); if (lane >= 32) v = max(v, t);
+    return v;
+}
+
+// value of lane-1 (wave_shr:1); lane 0 gets `first`
+__device__ __forceinline__ double wave_shr1(double v, int lane, double first) {
+    const double t = dpp_d<0x138>(v);
+    return lane == 0 ? first : t;
+}
+__device__ __forceinline__ int wave_shr1(int v, int lane, int first) {
+    const int t = dpp_i<0x138>(v);
+    return lane == 0 ? first : t;
+}
+
+__device__ __forceinline__ double readlane(double v, int j) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), j);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), j);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ float readlane(float v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+__device__ __forceinline__ int readlane(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+}  // namespace ofs
+
+// internal launchers implemented in aa_fast.hip (C++ linkage, not part of the ABI)
+struct AaFastArgs {
+    const void* x;
+    int64_t B, T;
+    int32_t L;
+    void* P; void* R; void* M; uint8_t* valid;
+    int32_t detect; double thr; int32_t hyst; double fs;
+    int32_t max_ev; int32_t* n_ev; int64_t* ev_i; double* ev_r;
+};
+// returns 1 if the fast path handled the call (launched), 0 if not applicable, <0 on error
+int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st);
