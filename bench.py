@@ -25,7 +25,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 
-from ofdm_sync_amd import _lib, synth  # noqa: E402
+from ofdm_sync_amd import _lib, shard, synth  # noqa: E402
 
 METRIC = "complex Msamples/s through S&C metric kernel @ batch=65536; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
@@ -86,18 +86,15 @@ def pmc_traffic(workload_key: str):
 
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    info = shard.rank_info()
+    rank, world, local = info.rank, info.world, info.local_rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    dist = shard.init("nccl", dev)          # RCCL; control plane only (barrier + MAX of times)
 
+    # weak scaling: every rank owns its own B-stream shard (independent streams)
     B, T, L, E = a.batch, a.T, a.L, a.max_events
-    x = synth.make_aa_batch(B, T, L, seed=2026 + rank, device=dev)
+    x = synth.make_aa_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev)
     P = torch.empty((B, T), dtype=torch.complex64, device=dev)
     R = torch.empty((B, T), dtype=torch.float32, device=dev)
     M = torch.empty((B, T), dtype=torch.float32, device=dev)
@@ -134,10 +131,7 @@ def main():
     if dist:
         dist.barrier()
     ms = e0.elapsed_time(e1)
-    ms_t = torch.tensor([ms], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(ms_t, op=dist.ReduceOp.MAX)
-    ms_max = float(ms_t.item())
+    ms_max = shard.max_over_ranks(ms, dist, dev)
     ms_per_step = ms_max / a.steps
 
     # algorithmic bytes of one launch

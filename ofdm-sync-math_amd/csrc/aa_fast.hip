@@ -26,6 +26,16 @@ using namespace ofs;
 namespace {
 
 constexpr int FAST_WG = 256;      // 4 waves = 4 independent streams per workgroup
+
+// occupancy bound (min waves per SIMD) of the fast kernel; tuning builds set -DOFS_FAST_WAVES=N
+#ifndef OFS_FAST_WAVES
+#define OFS_FAST_WAVES 0
+#endif
+#if OFS_FAST_WAVES > 0
+#define OFS_FAST_BOUNDS __launch_bounds__(FAST_WG, OFS_FAST_WAVES)
+#else
+#define OFS_FAST_BOUNDS __launch_bounds__(FAST_WG)
+#endif
 constexpr int TMAX = 1024;        // stream length handled by the fast path
 constexpr int NOKEY = 1 << 20;
 
@@ -47,36 +57,44 @@ __device__ __forceinline__ double scan_add(double v) {
 }
 __device__ __forceinline__ double shr1z(double v) { return dppz<0x138>(v); }   // wave_shr:1, lane 0 <- 0
 
-template <int NA, int E, int MR>
-__global__ __launch_bounds__(FAST_WG) void aa_fast_kernel(AaFastArgs a) {
+// Stream staging: the wave DMAs its whole stream into a private 8 KiB LDS slice
+// (global_load_lds_dwordx4: no VGPRs, one contiguous 1 KiB per wave-instruction) and reads
+// rows back with conflict-free ds_read_b128 when it needs them — the current row and the row
+// MR back for the lagged product — so samples never occupy registers across rows.
+template <int E, int MR>
+__global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;                 // samples per row
     constexpr int RW = TMAX / RL;              // rows per stream
     constexpr int L = MR * RL;
     constexpr int V4 = E / 2;                  // float4 (2 samples) per lane per row
     static_assert(MR >= 1 && MR <= RW, "window must fit the stream tile");
+    __shared__ float4 lds[FAST_WG / 64][RW * V4][64];
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * (FAST_WG / 64) + (threadIdx.x >> 6);
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * (FAST_WG / 64) + w;
     if (b >= a.B) return;
     const int T = (int)a.T;
-    const float4* xin = reinterpret_cast<const float4*>(a.x);
-
-    // ---- every load of the stream up front: RW x V4 x NA dwordx4 per lane ----
-    float4 xv[NA][RW][V4];
+    {
+        const float2* xs = reinterpret_cast<const float2*>(a.x) + b * a.T;
 #pragma unroll
-    for (int k = 0; k < RW; ++k)
+        for (int k = 0; k < RW; ++k)
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                int n = RL * k + E * lane + 2 * j;
+                n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
+                __builtin_amdgcn_global_load_lds((const void*)(xs + n),
+                                                 (__attribute__((address_space(3))) void*)&lds[w][k * V4 + j][0],
+                                                 16, 0, 0);
+            }
+    }
+    auto xrow = [&](int k, float (&re)[E], float (&im)[E]) {
 #pragma unroll
         for (int j = 0; j < V4; ++j) {
-            const int n = RL * k + E * lane + 2 * j;
-#pragma unroll
-            for (int br = 0; br < NA; ++br)
-                xv[br][k][j] = (n < T) ? xin[((b * NA + br) * a.T + n) >> 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const bool ok = RL * k + E * lane + 2 * j < T;
+            const float4 v = lds[w][k * V4 + j][lane];
+            re[2 * j] = ok ? v.x : 0.f; im[2 * j] = ok ? v.y : 0.f;
+            re[2 * j + 1] = ok ? v.z : 0.f; im[2 * j + 1] = ok ? v.w : 0.f;
         }
-    auto xat = [&](int br, int k, int e, double& re, double& im) {
-        float fr, fi;
-        const float4 v = xv[br][k][e >> 1];
-        if (e & 1) { fr = v.z; fi = v.w; } else { fr = v.x; fi = v.y; }
-        asm volatile("" : "+v"(fr), "+v"(fi));   // keep samples fp32 in registers: convert at use
-        re = fr; im = fi;
     };
 
     float sR[MR][E], sI[MR][E], sE[MR][E];      // retained in-window suffixes (ring by k % MR)
@@ -103,70 +121,65 @@ __global__ __launch_bounds__(FAST_WG) void aa_fast_kernel(AaFastArgs a) {
     float* Pout = reinterpret_cast<float*>(a.P);
     float* Rout = reinterpret_cast<float*>(a.R);
     float* Mout = reinterpret_cast<float*>(a.M);
+    const float floor_ = 1e-6f * (float)L;
 
 #pragma unroll
     for (int k = 0; k < RW; ++k) {
         if (RL * k < T) {                                       // wave-uniform row guard
             const int nb = RL * k + E * lane;                   // first sample of this lane
-            // ---- pass 1: lane totals of products / energies, wave scan ----
-            double tR = 0.0, tI = 0.0, tE = 0.0;
+            // ---- lagged products x[n]·conj(x[n-L]) and energies, fp32 ----
+            float aR[E], aI[E], aE[E];
+            {
+                float cr[E], ci[E];
+                xrow(k, cr, ci);
 #pragma unroll
-            for (int e = 0; e < E; ++e)
+                for (int e = 0; e < E; ++e) aE[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                if (k >= MR) {
+                    float dr[E], di[E];
+                    xrow(k - MR, dr, di);
 #pragma unroll
-                for (int br = 0; br < NA; ++br) {
-                    double xr, xi;
-                    xat(br, k, e, xr, xi);
-                    tE += xr * xr + xi * xi;
-                    if (k >= MR) {
-                        double dr, di;
-                        xat(br, k - MR, e, dr, di);
-                        tR += xr * dr + xi * di;                 // x[n]·conj(x[n-L])
-                        tI += xi * dr - xr * di;
+                    for (int e = 0; e < E; ++e) {
+                        aR[e] = fmaf(cr[e], dr[e], ci[e] * di[e]);
+                        aI[e] = fmaf(ci[e], dr[e], -(cr[e] * di[e]));
                     }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; }
                 }
-            const double iR = scan_add(tR), iI = scan_add(tI), iE = scan_add(tE);
-            double rR = shr1z(iR), rI = shr1z(iI), rE = shr1z(iE);   // exclusive in-row prefix
+            }
+            // ---- in-lane partials, each summing only the terms it stands for:
+            //      forward f[e] = sum_{e'<=e} a[e'], backward g[e] = sum_{e'>e} a[e'] ----
+            float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
+            fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+#pragma unroll
+            for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
+            gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+#pragma unroll
+            for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+            // ---- lane totals: fp64 DPP wave scan, row totals, rows inside the window ----
+            const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
             const double totR = readlane(iR, 63), totI = readlane(iI, 63), totE = readlane(iE, 63);
+            const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);   // lanes < l
+            const float uR = (float)(totR - iR), uI = (float)(totI - iI), uE = (float)(totE - iE);  // lanes > l
             Cr[k + 1] = Cr[k] + totR; Ci[k + 1] = Ci[k] + totI; Ce[k + 1] = Ce[k] + totE;
-            // rows strictly inside the window (k >= MR) or everything before row k (k < MR)
-            const double fR = (k >= MR) ? (Cr[k] - Cr[k - MR + 1]) : Cr[k];
-            const double fI = (k >= MR) ? (Ci[k] - Ci[k - MR + 1]) : Ci[k];
-            const double fE = (k >= MR) ? (Ce[k] - Ce[k - MR + 1]) : Ce[k];
+            const float wR = (float)((k >= MR) ? (Cr[k] - Cr[k - MR + 1]) : Cr[k]);
+            const float wI = (float)((k >= MR) ? (Ci[k] - Ci[k - MR + 1]) : Ci[k]);
+            const float wE = (float)((k >= MR) ? (Ce[k] - Ce[k - MR + 1]) : Ce[k]);
 
-            // ---- pass 2: recompute products, window sums, metric, outputs ----
-            float pf[E][2], mf[E], pmf[E], rf[E], nsR[E], nsI[E], nsE[E];
+            // ---- window sums  P = suffix(row k-MR) + rows between + prefix(row k) ----
+            float pf[E][2], mf[E], pmf[E], rf[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                double aR = 0.0, aI = 0.0, aE = 0.0;
-#pragma unroll
-                for (int br = 0; br < NA; ++br) {
-                    double xr, xi;
-                    xat(br, k, e, xr, xi);
-                    aE += xr * xr + xi * xi;
-                    if (k >= MR) {
-                        double dr, di;
-                        xat(br, k - MR, e, dr, di);
-                        aR += xr * dr + xi * di;
-                        aI += xi * dr - xr * di;
-                    }
-                }
-                rR += aR; rI += aI; rE += aE;                   // inclusive in-row prefix
-                double PR = rR + fR, PI = rI + fI, RR = rE + fE;
-                if (k >= MR) {
-                    PR += (double)sR[k % MR][e]; PI += (double)sI[k % MR][e]; RR += (double)sE[k % MR][e];
-                }
-                nsR[e] = (float)(totR - rR); nsI[e] = (float)(totI - rI); nsE[e] = (float)(totE - rE);
-                const double pm = PR * PR + PI * PI;
-                double m = 0.0;
-                if (k >= MR && RR > 1e-6 * (double)L) {
-                    m = pm / (RR * RR);
-                    m = m < 1.0 ? m : 1.0;
-                }
-                pf[e][0] = (float)PR; pf[e][1] = (float)PI;
-                rf[e] = (float)RR; mf[e] = (float)m; pmf[e] = (float)pm;
+                float PR = wR + (xR + fR[e]);
+                float PI = wI + (xI + fI[e]);
+                float RR = wE + (xE + fE[e]);
+                if (k >= MR) { PR += sR[k % MR][e]; PI += sI[k % MR][e]; RR += sE[k % MR][e]; }
+                sR[k % MR][e] = uR + gR[e]; sI[k % MR][e] = uI + gI[e]; sE[k % MR][e] = uE + gE[e];
+                const float pm = fmaf(PR, PR, PI * PI);
+                float m = 0.f;
+                if (k >= MR && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
+                pf[e][0] = PR; pf[e][1] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
             }
-#pragma unroll
-            for (int e = 0; e < E; ++e) { sR[k % MR][e] = nsR[e]; sI[k % MR][e] = nsI[e]; sE[k % MR][e] = nsE[e]; }
 
             const int64_t o = b * a.T + nb;
 #pragma unroll
@@ -214,29 +227,22 @@ __global__ __launch_bounds__(FAST_WG) void aa_fast_kernel(AaFastArgs a) {
                 carry_last = readlane(W, 63);
 
                 auto seg_reduce = [&](int lo, int hi) {        // first argmax of |P|² on keys [lo, hi]
-                    float c[E];
-                    float lm = -1.f;
+                    // per-lane best (strict >: lowest element wins ties), then across lanes
+                    float lv = -1.f, lpr = 0.f, lpi = 0.f, lm = 0.f;
+                    int lk = NOKEY;
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
                         const int key = E * lane + e;
-                        c[e] = (nb + e < T && key >= lo && key <= hi) ? pmf[e] : -1.f;
-                        lm = fmaxf(lm, c[e]);
+                        const bool in = nb + e < T && key >= lo && key <= hi;
+                        if (in && pmf[e] > lv) { lv = pmf[e]; lk = key; lpr = pf[e][0]; lpi = pf[e][1]; lm = mf[e]; }
                     }
-                    const float vmax = wave_max(lm);
-                    int kk = NOKEY;
-#pragma unroll
-                    for (int e = E - 1; e >= 0; --e)
-                        if (c[e] == vmax) kk = E * lane + e;
-                    kk = wave_min(kk);
+                    const float vmax = wave_max(lv);
+                    const int kk = wave_min(lv == vmax ? lk : NOKEY);
                     if (vmax > bpm && kk != NOKEY) {
-                        const int ln = kk / E, es = kk % E;
-                        float sel_pr = pf[0][0], sel_pi = pf[0][1], sel_m = mf[0];
-#pragma unroll
-                        for (int e = 1; e < E; ++e)
-                            if (es == e) { sel_pr = pf[e][0]; sel_pi = pf[e][1]; sel_m = mf[e]; }
-                        bpr = readlane(sel_pr, ln);
-                        bpi = readlane(sel_pi, ln);
-                        bm = readlane(sel_m, ln);
+                        const int ln = kk / E;
+                        bpr = readlane(lpr, ln);
+                        bpi = readlane(lpi, ln);
+                        bm = readlane(lm, ln);
                         bpm = vmax;
                         bidx = RL * k + kk;
                     }
@@ -277,29 +283,28 @@ __global__ __launch_bounds__(FAST_WG) void aa_fast_kernel(AaFastArgs a) {
     }
 }
 
-template <int NA, int E, int MR>
+template <int E, int MR>
 int launch(const AaFastArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + 3) / 4;
-    hipLaunchKernelGGL((aa_fast_kernel<NA, E, MR>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
+    hipLaunchKernelGGL((aa_fast_kernel<E, MR>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
-template <int NA, int E, int MR = 1>
+template <int E, int MR = 1>
 int launch_mr(int mr, const AaFastArgs& a, hipStream_t st) {
     if constexpr (MR > TMAX / (64 * E)) {
         return 0;
     } else {
-        if (mr == MR) return launch<NA, E, MR>(a, st);
-        return launch_mr<NA, E, MR + 1>(mr, a, st);
+        if (mr == MR) return launch<E, MR>(a, st);
+        return launch_mr<E, MR + 1>(mr, a, st);
     }
 }
 
-template <int NA>
 int launch_e(int E, int mr, const AaFastArgs& a, hipStream_t st) {
     switch (E) {
-        case 2: return launch_mr<NA, 2>(mr, a, st);
-        case 4: return launch_mr<NA, 4>(mr, a, st);
-        case 8: return launch_mr<NA, 8>(mr, a, st);
+        case 2: return launch_mr<2>(mr, a, st);
+        case 4: return launch_mr<4>(mr, a, st);
+        case 8: return launch_mr<8>(mr, a, st);
     }
     return 0;
 }
@@ -312,7 +317,7 @@ int pick_e(int L) {
         forced = s ? atoi(s) : 0;
     }
     if (forced == 2 || forced == 4 || forced == 8) return (L % (64 * forced) == 0) ? forced : 0;
-    for (int e : {8, 4, 2})
+    for (int e : {4, 2, 8})
         if (L % (64 * e) == 0) return e;
     return 0;
 }
@@ -321,11 +326,11 @@ int pick_e(int L) {
 
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
     if (fmt != OFS_C64 || precision != OFS_FP32) return 0;
-    if (n_ant < 1 || n_ant > 2) return 0;
+    if (n_ant != 1) return 0;
     if (a.T < 2 || a.T > TMAX || (a.T & 1)) return 0;
     if (a.L < 128 || a.L > TMAX) return 0;
     const int E = pick_e(a.L);
     if (!E) return 0;
     const int mr = a.L / (64 * E);
-    return n_ant == 1 ? launch_e<1>(E, mr, a, st) : launch_e<2>(E, mr, a, st);
+    return launch_e(E, mr, a, st);
 }

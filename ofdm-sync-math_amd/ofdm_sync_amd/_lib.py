@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libofdmsync.so")
+LIB_PATH = os.environ.get("OFS_LIB") or os.path.join(_HERE, "libofdmsync.so")   # OFS_LIB: tuning builds
 
 # input formats / precisions / status (include/ofdmsync.h)
 C64, C128, CI16 = 0, 1, 2
