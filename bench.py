@@ -72,6 +72,13 @@ def cpu_baseline(x_dev: torch.Tensor, L: int, threads: int, gpu_M: torch.Tensor)
                 max_abs_err_M_vs_gpu=err)
 
 
+def kernel_label(plan: int) -> str:
+    if plan >= 1000:
+        e, mr = (plan - 1000) // 10, (plan - 1000) % 10
+        return f"aa_fast_kernel<E={e},MR={mr}> (wave per stream, LDS-DMA staged, fused metric + events)"
+    return {1: "win_kernel<C64,fp32,AA> (fused events)", 2: "win_kernel<C64,fp32,AA> + aa_events_kernel"}.get(plan, str(plan))
+
+
 def pmc_traffic(workload_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this
     workload (collected in separate --pmc passes, corrected per MI355X_MICROARCH.md §HBM)."""
@@ -166,7 +173,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "aa_fast_kernel<NA=1,E=8,MR=1> (wave per stream, fused metric + events)",
+                         "kernel": kernel_label(lib.ofs_aa_plan(_lib.C64, _lib.FP32, 1, T, L)),
                          "alg_bytes_per_launch": alg_bytes,
                          "avg_launch_ms": round(ms / a.steps, 5)},
             "events_per_stream": round(float(n_ev.float().mean().item()), 3),

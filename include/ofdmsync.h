@@ -62,6 +62,16 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
                       void* stream);
 
 /*
+ * Which kernel ofs_aa_detect dispatches a shape to (pure query, no launch):
+ *   1000 + 10*E + MR : register-resident wave-per-stream fast path (E samples per lane,
+ *                      L = 64*E*MR), complex64 / OFS_FP32 / one antenna / even T <= 1024;
+ *   1                : general LDS engine, events fused (stream fits one tile);
+ *   2                : general LDS engine, tiled, events in a second pass over P/M;
+ *   <0               : invalid arguments or window too long (as ofs_aa_detect would return).
+ */
+int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T, int32_t L);
+
+/*
  * Schmidl-Cox half-symbol metric, reference index convention d = 0 .. T-N.
  * r_mode 0 replaces sc.sc_streaming_metric (sc.py:42-78; R = second-half energy);
  * r_mode 1 replaces combined_sc_min.schmidl_cox_streaming_metric (combined_sc_min.py:116-164;

@@ -324,13 +324,18 @@ int pick_e(int L) {
 
 }  // namespace
 
-int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
+int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
     if (fmt != OFS_C64 || precision != OFS_FP32) return 0;
     if (n_ant != 1) return 0;
-    if (a.T < 2 || a.T > TMAX || (a.T & 1)) return 0;
-    if (a.L < 128 || a.L > TMAX) return 0;
-    const int E = pick_e(a.L);
+    if (T < 2 || T > TMAX || (T & 1)) return 0;
+    if (L < 128 || L > TMAX) return 0;
+    const int E = pick_e(L);
     if (!E) return 0;
-    const int mr = a.L / (64 * E);
-    return launch_e(E, mr, a, st);
+    return 10 * E + L / (64 * E);
+}
+
+int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
+    const int plan = ofs_aa_fast_plan(fmt, precision, n_ant, a.T, a.L);
+    if (!plan) return 0;
+    return launch_e(plan / 10, plan % 10, a, st);
 }

@@ -803,6 +803,19 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
     return OFS_OK;
 }
 
+int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T, int32_t L) {
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || n_ant < 1 || T < 0 || L < 1) return OFS_EINVAL;
+    const int fp = ofs_aa_fast_plan(in_fmt, precision, n_ant, T, L);
+    if (fp) return 1000 + fp;
+    if (2 * (int64_t)L - 1 > 0x3fffffff) return OFS_ETOOLONG;
+    Plan p;
+    const int lo = -(int)(2 * (int64_t)L - 1);
+    const int rc = precision == OFS_FP64 ? make_plan<double>(T > 0 ? T : 1, T > 0 ? T : 1, lo, 0, 3, true, p)
+                                         : make_plan<float>(T > 0 ? T : 1, T > 0 ? T : 1, lo, 0, 3, false, p);
+    if (rc) return rc;
+    return p.n_chunks > 1 ? 2 : 1;
+}
+
 int32_t ofs_sc_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                       int32_t symbol_len, int32_t r_mode, int32_t precision,
                       void* M, void* P, void* R, void* stream) {

@@ -87,3 +87,5 @@ struct AaFastArgs {
 };
 // returns 1 if the fast path handled the call (launched), 0 if not applicable, <0 on error
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st);
+// 10*E + MR of the fast kernel a shape dispatches to, 0 if the general engine handles it
+int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L);

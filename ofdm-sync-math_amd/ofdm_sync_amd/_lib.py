@@ -30,6 +30,7 @@ def _declare(lib):
         "ofs_status_string": (ctypes.c_char_p, [c_int32]),
         "ofs_aa_detect": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P, P,
                                     P, c_int32, c_double, c_int32, c_double, c_int32, P, P, P, P]),
+        "ofs_aa_plan": (c_int32, [c_int32, c_int32, c_int32, c_int64, c_int32]),
         "ofs_sc_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
                                     c_int32, P, P, P, P]),
         "ofs_minn_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,

@@ -373,3 +373,41 @@ def test_aa_fp32_full_batch_properties():
     assert torch.allclose(out2.R, 4 * out.R, rtol=1e-5)
     # every stream has its gate open at the end (correlated second half) -> >= 1 event
     assert bool((out.n_events >= 1).all())
+
+
+# ------------------------------------------------------- fast path (aa_fast_kernel) ------------
+@pytest.mark.parametrize("L", [128, 256, 384, 512, 640, 768, 896, 1024])
+@pytest.mark.parametrize("T", [130, 512, 998, 1024])
+def test_aa_fast_path_sweep(L, T):
+    """Every (E, MR) instantiation of the wave-per-stream kernel against the oracle on the same
+    complex64 samples; the dispatch is asserted to be the fast path."""
+    plan = _lib.lib().ofs_aa_plan(_lib.C64, _lib.FP32, 1, T, L)
+    assert plan >= 1000, plan
+    rng = np.random.default_rng(L * 7 + T)
+    B = 9
+    x = (rng.standard_normal((B, 1, T)) + 1j * rng.standard_normal((B, 1, T))) * 0.3
+    for b in range(B):                      # [A][A] bursts at random offsets, some streams quiet
+        if b % 3 == 2 or T < 2 * L:
+            continue
+        s = int(rng.integers(0, T - 2 * L + 1))
+        a = rng.standard_normal(L) + 1j * rng.standard_normal(L)
+        x[b, 0, s:s + L] += a
+        x[b, 0, s + L:s + 2 * L] += a
+    x = x.astype(np.complex64)
+    out = sync_aa.aa_detect_streaming_batched(torch.from_numpy(x).cuda(), L=L, threshold=0.3, hysteresis=32)
+    for b in range(B):
+        Pr, Rr, Mr, vr, ei, er = O.aa_detect(x[b].astype(np.complex128), L, 0.3, 32)
+        assert np.max(np.abs(out.M[b].cpu().numpy() - Mr)) < 1e-6
+        assert relerr(out.P[b].cpu().numpy(), Pr) < 1e-5 and relerr(out.R[b].cpu().numpy(), Rr) < 1e-5
+        assert np.array_equal(out.valid[b].cpu().numpy(), vr)
+        n = int(out.n_events[b])
+        assert n == len(ei)
+        gi = out.ev_int[b, :n].cpu().numpy()
+        assert np.all(np.abs(gi[:, 1:3] - ei[:, 1:3]) <= 1)
+        assert np.all(np.abs(gi[:, 0] - ei[:, 0]) <= 2)
+        assert np.array_equal(gi[:, 3], gi[:, 0] - 2 * L + 1)
+
+
+def test_aa_fast_path_is_used_for_the_benchmark_shape():
+    assert _lib.lib().ofs_aa_plan(_lib.C64, _lib.FP32, 1, 1024, 512) >= 1000
+    assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, 1, 1024, 512) in (1, 2)
