@@ -24,6 +24,8 @@ __all__ = [
     "aa_metric", "aa_events", "aa_detect",
     "sc_metric", "comb_sc_metric", "minn_metric",
     "minn_rtl_metric", "detect_minn_rtl", "cp_cfo",
+    "park_metric", "zc_template", "zc_freq_metric", "pss_symbol", "matched_filter",
+    "normalize_correlation", "zc_combined", "zc_streaming_detection", "detect_zc_peaks",
 ]
 
 
@@ -301,3 +303,181 @@ def cp_cfo(rx, start, n_fft, cp_len, fs_hz):
     b = x[:, start + n_fft:start + n_fft + cp_len]
     P = np.sum(a * np.conj(b))
     return float(-np.angle(P) * fs_hz / (2 * np.pi * n_fft)), complex(P)
+
+
+# ---------------------------------------------------------------------------------------
+# park.park_streaming_metric (park.py:64-114)
+# ---------------------------------------------------------------------------------------
+def park_metric(rx, N):
+    """(ds, M, P, E) of park.park_streaming_metric with park.N_FFT = N.
+
+    half = N//2; ds = [half, T-half-1]                               (:76-96)
+    P(d) = sum_br sum_{k<half} x[d-k] * x[d+k]   (no conjugate)      (:103-107)
+    E(d) = sum_br sum_{k<half} |x[d+k]|^2                            (:108)
+    M = |P|^2 / max(E, 1e-12)^2                                      (:112-113)
+    Vectorised over d, looping over k (same products, summed in k order per branch).
+    """
+    x = _as2d(rx)
+    nb, T = x.shape
+    half = N // 2
+    if half == 0 or T < 2 * half + 1:
+        return (np.zeros(0, dtype=int), np.zeros(0), np.zeros(0, np.complex128), np.zeros(0))
+    ds = np.arange(half, T - half)
+    P = np.zeros(ds.size, np.complex128)
+    E = np.zeros(ds.size)
+    for b in range(nb):
+        xb = x[b]
+        Pb = np.zeros(ds.size, np.complex128)
+        for k in range(half):
+            Pb += xb[ds - k] * xb[ds + k]
+        e = np.abs(xb) ** 2
+        Eb = (_pref(e)[ds + half] - _pref(e)[ds])
+        P += Pb
+        E += Eb
+    M = np.abs(P) ** 2 / np.maximum(E, 1e-12) ** 2
+    return ds, M, P, E
+
+
+# ---------------------------------------------------------------------------------------
+# zc_freq.compute_frequency_metric (zc_freq.py:62-99) + make_pss_frequency_template (:54-59)
+# ---------------------------------------------------------------------------------------
+def zc_template(length=62, root=25):
+    """(bin_indices, template_bins, energy): centered +-1..+-length/2 (core.py:13-18), ZC
+    root/length sequence exp(-j*pi*r*n*(n+1)/len) (zc_freq.py:37-39)."""
+    half = length // 2
+    idx = np.concatenate((np.arange(-half, 0), np.arange(1, half + 1)))
+    n = np.arange(length)
+    t = np.exp(-1j * np.pi * root * n * (n + 1) / length)
+    return idx, t, float(np.sum(np.abs(t) ** 2))
+
+
+def zc_freq_metric(rx, N, cp, bin_indices, template_bins, template_energy):
+    """metric[off] for off in [0, T-(N+cp)]: window x[off+cp : off+cp+N] per branch,
+    bins = fftshift(fft(window))[(N/2 + idx) % N] == fft(window)[idx % N];
+    metric = |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum |bins|^2, 1e-12).
+    The 62 DFT bins are evaluated as a direct DFT (matrix product) instead of a full FFT;
+    identical mathematics, agreement ~1e-13 relative.  Raises ValueError when too short (:76-78).
+    """
+    x = _as2d(rx)
+    nb, T = x.shape
+    noff = T - (N + cp) + 1
+    if noff <= 0:
+        raise ValueError("Received stream is shorter than a single OFDM symbol.")
+    k = np.asarray(bin_indices) % N
+    W = np.exp(-2j * np.pi * np.outer(np.arange(N), k) / N)            # [N][62]
+    t = np.asarray(template_bins, np.complex128)
+    corr = np.zeros(noff, np.complex128)
+    en = np.zeros(noff)
+    CH = 2048
+    for b in range(nb):
+        win = np.lib.stride_tricks.sliding_window_view(x[b, cp:], N)[:noff]
+        for o0 in range(0, noff, CH):
+            bins = win[o0:o0 + CH] @ W
+            corr[o0:o0 + CH] += bins @ np.conj(t)
+            en[o0:o0 + CH] += np.sum(np.abs(bins) ** 2, axis=1)
+    return np.abs(corr) ** 2 / np.maximum(template_energy * en, 1e-12)
+
+
+# ---------------------------------------------------------------------------------------
+# ZC matched filter: zc_v2.py:244-271 and the inline combiner of zc.py:106-126
+# ---------------------------------------------------------------------------------------
+def pss_symbol(N, length=62, root=25):
+    """zc_v2.build_pss_symbol(include_cp=False) / zc.build_pss_symbol(False) for N_FFT = N:
+    ZC on centered bins, ifft(ifftshift(.)), scaled to unit mean power (core.py:21-40)."""
+    idx, t, _ = zc_template(length, root)
+    spec = np.zeros(N, np.complex128)
+    spec[(N // 2 + idx) % N] = t
+    td = np.fft.ifft(np.fft.ifftshift(spec))
+    p = np.mean(np.abs(td) ** 2)
+    return td if p == 0 else td / np.sqrt(p)
+
+
+def matched_filter(x, ref):
+    """np.convolve(x, conj(ref[::-1]), 'full') (zc_v2.py:244-254)."""
+    return np.convolve(np.asarray(x, np.complex128), np.conj(np.asarray(ref)[::-1]))
+
+
+def _window_energy_full(x, n):
+    """np.convolve(|x|^2, ones(n), 'full') as a prefix difference (length T+n-1)."""
+    e = np.abs(np.asarray(x)) ** 2
+    p = _pref(e)
+    T = e.size
+    i = np.arange(T + n - 1)
+    return p[np.minimum(i + 1, T)] - p[np.maximum(i + 1 - n, 0)]
+
+
+def normalize_correlation(corr, x, ref):
+    """corr / (sqrt(E_ref) * sqrt(max(window_energy, 1e-12))) (zc_v2.py:257-271)."""
+    ref = np.asarray(ref)
+    e = _window_energy_full(x, ref.size)
+    return corr / (np.sqrt(np.sum(np.abs(ref) ** 2)) * np.sqrt(np.maximum(e, 1e-12)))
+
+
+def zc_combined(rx, ref):
+    """zc.py:106-126: sum_br conv(x, conj(ref[::-1])) / (|ref| * sqrt(max(sum_br E, 0) + 1e-12))."""
+    x = _as2d(rx)
+    ref = np.asarray(ref)
+    num = sum(matched_filter(b, ref) for b in x)
+    pw = sum(_window_energy_full(b, ref.size) for b in x)
+    return num / (np.sqrt(np.sum(np.abs(ref) ** 2)) * np.sqrt(np.maximum(pw, 0.0) + 1e-12))
+
+
+def zc_streaming_detection(corr_mag, window_size, thresh_value, thresh_frac_bits, min_corr_mag):
+    """zc_v2.zc_streaming_detection (zc_v2.py:300-346), RunningSum (:219-238) restated
+    literally (sequential float64 add/subtract, valid once W samples have been pushed)."""
+    c = np.asarray(corr_mag, np.float64)
+    n = c.size
+    W = max(1, int(window_size))
+    local = np.zeros(n)
+    valid = np.zeros(n, bool)
+    acc = 0.0
+    for i in range(n):
+        if i >= W:
+            acc = acc + c[i] - c[i - W]
+            valid[i] = True
+        else:
+            acc = acc + c[i]
+        local[i] = acc
+    cs = c * float(1 << thresh_frac_bits)
+    ts = local * float(thresh_value)
+    above = valid & (cs >= ts) & (c >= min_corr_mag)
+    return dict(corr_mag=c, local_sum=local, corr_scaled=cs, thresh_scaled=ts,
+                above_threshold=above, metric_valid=valid)
+
+
+def detect_zc_peaks(corr_mag, above, valid, reference_length, hysteresis):
+    """Literal restatement of zc_v2.detect_zc_peaks (zc_v2.py:374-446).
+
+    Returns (events[k,4] = peak_index, gate_start, gate_end, detected_start,
+             peak_values[k], gate_mask)."""
+    n = len(corr_mag)
+    mask = np.zeros(n, bool)
+    evs, vals = [], []
+    gate_open = False
+    gate_start = peak_index = low = 0
+    peak_value = 0.0
+    hyst_limit = max(0, hysteresis - 1)
+    for i in range(n):
+        if not valid[i]:
+            continue
+        v = corr_mag[i]
+        if not gate_open:
+            if above[i]:
+                gate_open, gate_start, peak_index, peak_value, low = True, i, i, v, 0
+        else:
+            mask[i] = True
+            if v > peak_value:
+                peak_value, peak_index = v, i
+            if above[i]:
+                low = 0
+            elif hysteresis == 0 or low >= hyst_limit:
+                evs.append((peak_index, gate_start, i, max(0, peak_index - reference_length + 1)))
+                vals.append(peak_value)
+                gate_open, peak_value, low = False, 0.0, 0
+            else:
+                low += 1
+    if gate_open:
+        evs.append((peak_index, gate_start, n, max(0, peak_index - reference_length + 1)))
+        vals.append(peak_value)
+        mask[gate_start:n] = True
+    return np.array(evs, np.int64).reshape(-1, 4), np.array(vals, np.float64), mask

@@ -17,6 +17,11 @@ Reference entry points exercised (file:line into /root/reference):
   minn_rtl.minn_rtl_streaming_metric  minn_rtl.py:667-733
   minn_rtl.detect_minn_rtl             minn_rtl.py:750-825
   core.estimate_cfo_from_cp            core.py:179-196
+  park.park_streaming_metric           park.py:64-114     (park.N_FFT overridden per case)
+  zc_freq.compute_frequency_metric     zc_freq.py:62-99   (zc_freq.N_FFT / CYCLIC_PREFIX overridden)
+  zc_v2.matched_filter_correlation / normalize_correlation / zc_streaming_detection /
+  detect_zc_peaks / detect_zc_preamble zc_v2.py:244-519
+  zc.py:106-126 inline combined matched filter (restated in gen_zc from the reference's lines)
 Input builders used only to synthesise realistic streams (not part of the parity surface):
   sync_aa.build_aa_preamble / apply_channel_multi_antenna / apply_cfo / quantize_adc,
   sc.build_sc_preamble, combined_sc_min.build_minn_preamble, minn_rtl.build_minn_preamble_generic,
@@ -41,8 +46,10 @@ def _import_reference():
     sys.path.insert(0, str(REF))
     os.chdir(tempfile.mkdtemp(prefix="ofs_golden_"))  # scripts write plots/ relative to cwd
     import core, channel, sc, minn, minn_rtl, combined_sc_min, sync_aa  # noqa: E401
+    import park, zc, zc_freq, zc_v2  # noqa: E401
     return dict(core=core, channel=channel, sc=sc, minn=minn, minn_rtl=minn_rtl,
-                combined=combined_sc_min, sync_aa=sync_aa)
+                combined=combined_sc_min, sync_aa=sync_aa, park=park, zc=zc, zc_freq=zc_freq,
+                zc_v2=zc_v2)
 
 
 def _events_aa(res):
@@ -234,6 +241,86 @@ def gen_cp_cfo(R, cases):
                            cfo_1br_cp256=cfo1, fs_1br=np.float64(15.36e6))
 
 
+def gen_park(R, cases):
+    pk = R["park"]
+    core = R["core"]
+    ch = R["channel"]
+    for N, T, seed in ((2048, 7000, 0), (256, 3000, 1), (64, 400, 2)):
+        old = pk.N_FFT
+        pk.N_FFT = N
+        try:
+            rng = np.random.default_rng(seed)
+            if N == 2048:
+                pre = pk.build_park_preamble(rng, include_cp=True)
+                tx = np.concatenate([np.zeros(1337, complex), pre, core.build_random_qpsk_symbol(rng)[0]])
+                rx = ch.apply_channel(tx, 10.0, rng, ch.load_measured_cir("cir1")[:2])[:, :T]
+            else:
+                rx = rng.standard_normal((2, T)) + 1j * rng.standard_normal((2, T))
+                h = N // 2
+                a = rng.standard_normal(h) + 1j * rng.standard_normal(h)
+                rx[:, 100:100 + h] += a[::-1] * 2          # symmetric structure around d = 100 + h
+                rx[:, 100 + h:100 + 2 * h] += a * 2
+            ds, M, P, E = pk.park_streaming_metric(rx)
+        finally:
+            pk.N_FFT = old
+        cases[f"park_N{N}"] = dict(kind="park", x=rx, N=np.int64(N), ds=ds, M=M, P=P, E=E)
+
+
+def gen_zc(R, cases):
+    zf = R["zc_freq"]
+    z2 = R["zc_v2"]
+    zc = R["zc"]
+    core = R["core"]
+    ch = R["channel"]
+    # zc_freq.compute_frequency_metric (zc_freq.py:62-99); N_FFT / CYCLIC_PREFIX read at call time
+    for N, CP, T, seed in ((2048, 512, 4200, 0), (256, 64, 1500, 3)):
+        oldN, oldC = zf.N_FFT, zf.CYCLIC_PREFIX
+        zf.N_FFT, zf.CYCLIC_PREFIX = N, CP
+        try:
+            rng = np.random.default_rng(seed)
+            if N == 2048:
+                tx = np.concatenate([np.zeros(1337, complex), zf.build_pss_symbol(include_cp=True)])
+                rx = ch.apply_channel(tx, 10.0, rng, ch.load_measured_cir("cir1")[:2])[:, :T]
+            else:
+                rx = rng.standard_normal((2, T)) + 1j * rng.standard_normal((2, T))
+            bins, tmpl, energy = zf.make_pss_frequency_template()
+            metric = zf.compute_frequency_metric(rx, bins, tmpl, energy)
+        finally:
+            zf.N_FFT, zf.CYCLIC_PREFIX = oldN, oldC
+        cases[f"zcfreq_N{N}"] = dict(kind="zc_freq", x=rx, N=np.int64(N), CP=np.int64(CP), bins=bins,
+                                     template=tmpl, template_energy=np.float64(energy), metric=metric)
+    # zc_v2 matched filter / normaliser / streaming detection / gate (zc_v2.py:244-450), and the
+    # inline zc.py combined matched filter (zc.py:106-126, restated here statement for statement)
+    rng = np.random.default_rng(8)
+    ref = z2.build_pss_symbol(include_cp=False)
+    tx = np.concatenate([np.zeros(1500, complex), z2.build_pss_symbol(include_cp=True),
+                         core.build_random_qpsk_symbol(rng)[0]])
+    rx = core.apply_cfo(ch.apply_channel(tx, 10.0, rng, ch.load_measured_cir("cir1")[:2]), 1000.0,
+                        core.SAMPLE_RATE_HZ)[:, :6000]
+    corr = [z2.matched_filter_correlation(b, ref) for b in rx]
+    norm = [z2.normalize_correlation(c, b, ref) for c, b in zip(corr, rx)]
+    det = z2.detect_zc_preamble(rx)
+    st = det.state
+    ev = np.array([[e.peak_index, e.gate_start, e.gate_end, e.detected_start] for e in det.events],
+                  dtype=np.int64).reshape(-1, 4)
+    evv = np.array([e.peak_value for e in det.events], dtype=np.float64)
+    pss_reference = zc.build_pss_symbol(include_cp=False)
+    pss_conj = np.conj(pss_reference[::-1])
+    reference_norm = np.sqrt(np.sum(np.abs(pss_reference) ** 2))
+    window = np.ones(pss_reference.size, dtype=float)
+    num = sum(np.convolve(b, pss_conj) for b in rx)
+    pw = sum(np.convolve(np.abs(b) ** 2, window) for b in rx)
+    combined = num / (reference_norm * np.sqrt(np.maximum(pw, 0.0) + 1e-12))
+    cases["zc_mf"] = dict(kind="zc_mf", x=rx, ref=ref, corr=np.stack(corr), norm=np.stack(norm),
+                          zc_ref=pss_reference, zc_combined=combined,
+                          corr_mag=st.corr_mag, local_sum=st.local_sum, corr_scaled=st.corr_scaled,
+                          thresh_scaled=st.thresh_scaled, above_threshold=st.above_threshold,
+                          metric_valid=st.metric_valid, events=ev, peak_values=evv,
+                          gate_mask=det.gate_mask, window_size=np.int64(z2.CORR_WINDOW_SIZE),
+                          thresh_value=np.int64(z2.THRESH_VALUE), thresh_frac_bits=np.int64(z2.THRESH_FRAC_BITS),
+                          min_corr_mag=np.float64(z2.MIN_CORR_MAG), hysteresis=np.int64(z2.HYSTERESIS))
+
+
 def main():
     R = _import_reference()
     cases: dict[str, dict] = {}
@@ -242,6 +329,8 @@ def main():
     gen_combined(R, cases)
     gen_minn_rtl(R, cases)
     gen_cp_cfo(R, cases)
+    gen_park(R, cases)
+    gen_zc(R, cases)
     OUT.mkdir(parents=True, exist_ok=True)
     for name, d in cases.items():
         arrs = {k: (np.asarray(v) if not isinstance(v, str) else np.array(v)) for k, v in d.items()}

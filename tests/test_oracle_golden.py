@@ -71,6 +71,38 @@ def test_oracle_matches_reference_golden(path):
         assert np.allclose(c, d["cfo"], rtol=0, atol=1e-9)
         c1 = [O.cp_cfo(d["x"][0], int(s), 2048, 256, float(d["fs_1br"]))[0] for s in d["starts"]]
         assert np.allclose(c1, d["cfo_1br_cp256"], rtol=0, atol=1e-9)
+    elif kind == "park":
+        ds, M, P, E = O.park_metric(d["x"], int(d["N"]))
+        assert np.array_equal(ds, d["ds"])
+        assert np.allclose(P, d["P"], rtol=0, atol=1e-11 * float(np.abs(d["P"]).max()))
+        assert np.allclose(E, d["E"], rtol=1e-12, atol=0)
+        assert np.allclose(M, d["M"], rtol=1e-9, atol=1e-12)
+    elif kind == "zc_freq":
+        idx, t, et = O.zc_template()
+        assert np.array_equal(idx, d["bins"]) and np.allclose(t, d["template"], rtol=0, atol=1e-15)
+        assert et == float(d["template_energy"])
+        m = O.zc_freq_metric(d["x"], int(d["N"]), int(d["CP"]), idx, t, et)
+        assert np.allclose(m, d["metric"], rtol=1e-9, atol=1e-13)
+    elif kind == "zc_mf":
+        x, ref = d["x"], d["ref"]
+        N = ref.size
+        assert np.allclose(O.pss_symbol(N), ref, rtol=0, atol=1e-14)
+        assert np.allclose(O.pss_symbol(N), d["zc_ref"], rtol=0, atol=1e-14)
+        for b in range(x.shape[0]):
+            c = O.matched_filter(x[b], ref)
+            assert np.allclose(c, d["corr"][b], rtol=0, atol=1e-12)
+            assert np.allclose(O.normalize_correlation(c, x[b], ref), d["norm"][b], rtol=0, atol=1e-12)
+        assert np.allclose(O.zc_combined(x, ref), d["zc_combined"], rtol=0, atol=1e-12)
+        mag = np.abs(d["norm"].sum(axis=0))
+        assert np.allclose(mag, d["corr_mag"], rtol=0, atol=1e-15)
+        st = O.zc_streaming_detection(d["corr_mag"], int(d["window_size"]), int(d["thresh_value"]),
+                                      int(d["thresh_frac_bits"]), float(d["min_corr_mag"]))
+        for k in ("local_sum", "corr_scaled", "thresh_scaled", "above_threshold", "metric_valid"):
+            assert np.array_equal(st[k], d[k]), k        # literal recursion: bit-identical
+        ev, vals, mask = O.detect_zc_peaks(d["corr_mag"], st["above_threshold"], st["metric_valid"],
+                                           N, int(d["hysteresis"]))
+        assert np.array_equal(ev, d["events"]) and np.array_equal(vals, d["peak_values"])
+        assert np.array_equal(mask, d["gate_mask"])
     else:
         pytest.fail(kind)
 
