@@ -41,6 +41,14 @@ extern "C" {
 #define OFS_EINVAL       -1   /* bad argument (null required pointer, bad size, bad enum)  */
 #define OFS_ETOOLONG     -2   /* window/halo does not fit one workgroup's LDS tile          */
 #define OFS_EHIP         -3   /* kernel launch failed (hipGetLastError)                     */
+#define OFS_ESHORT       -4   /* stream shorter than one symbol (zc_freq.py:76-78 raises)   */
+
+/* ofs_zc_correlate modes */
+#define OFS_ZC_RAW        0   /* per-branch np.convolve(x, conj(ref[::-1]))                 */
+#define OFS_ZC_V2         1   /* zc_v2 detect_zc_preamble: sum of per-branch normalised corr */
+#define OFS_ZC_COMBINED   2   /* zc.py: sum_br corr / (|ref| sqrt(max(sum_br E, 0) + 1e-12)) */
+#define OFS_ZC_NORMALIZE  3   /* zc_v2.normalize_correlation(corr_in, x, ref), one branch    */
+#define OFS_ZC_SUM        4   /* sum_br raw corr (detect_zc_preamble, normalize=False)       */
 
 int32_t ofs_version(void);
 const char* ofs_status_string(int32_t status);
@@ -131,6 +139,65 @@ int32_t ofs_minn_rtl_gate(const double* corr_positive, const uint8_t* above_thre
 int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                    const int64_t* starts, int32_t n_fft, int32_t cp_len, double fs_hz,
                    double* P_out, double* cfo_out, void* stream);
+
+/*
+ * Park mirror-symmetry metric: replaces park.park_streaming_metric (park.py:64-114).
+ * half = N/2; outputs for d in [half, T-half-1], n_out = T - 2*half, laid out [B][n_out]:
+ *   P (c64|c128) = sum_br sum_{k<half} x[d-k]*x[d+k]; E (f32|f64) = sum_br sum_{k<half}|x[d+k]|^2;
+ *   M = |P|^2 / max(E, 1e-12)^2.  Each output nullable.  T < 2*half+1 or half == 0: nothing
+ *   to compute, returns OFS_OK (the reference returns empty arrays).  Tile + halo must fit
+ *   LDS: N <= 8190 (fp32) / 4094 (fp64), else OFS_ETOOLONG.
+ */
+int32_t ofs_park_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                        int32_t N, int32_t precision, void* M, void* P, void* E, void* stream);
+
+/*
+ * ZC matched filter / normaliser (fp64): replaces zc_v2.matched_filter_correlation
+ * (zc_v2.py:244-254), normalize_correlation (:257-271), the branch combine of
+ * detect_zc_preamble (:489-503) and the inline combiner of zc.py:106-126.
+ *   ref: [N] c128 (device); ref_energy = sum |ref|^2 (host scalar, as the reference computes it);
+ *   corr: c128 [B][n_br][T+N-1] (mode OFS_ZC_RAW) or [B][T+N-1] (other modes), nullable;
+ *   corr_mag: f64 |corr| with the same layout, nullable (one of corr / corr_mag required);
+ *   corr_in: c128 [B][T+N-1] raw correlation (OFS_ZC_NORMALIZE only, n_br must be 1).
+ *   N + 2048 samples of halo must fit LDS (N <= 6100).
+ */
+int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                         const void* ref, int32_t N, double ref_energy, int32_t mode,
+                         const void* corr_in, void* corr, double* corr_mag, void* stream);
+
+/*
+ * ZC frequency-domain metric (fp64): replaces zc_freq.compute_frequency_metric
+ * (zc_freq.py:62-99).  For off in [0, T-(N+cp)]: 62-bin DFT of x[off+cp : off+cp+N] at
+ * fftshift positions (N/2 + bin_indices) % N, metric = |sum_br vdot(t, bins)|^2 /
+ * max(E_t * sum_br sum |bins|^2, 1e-12).  bin_indices [n_bins] int32 and template_bins
+ * [n_bins] c128 are HOST pointers (n_bins <= 64); metric: [B][T-(N+cp)+1] f64 (device).
+ * n_br <= 4.  Returns OFS_ESHORT when T < N + cp (the reference raises ValueError).
+ */
+int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                           int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
+                           const double* template_bins, double template_energy, double* metric,
+                           void* stream);
+
+/*
+ * ZC CFAR + gate: replaces zc_v2.zc_streaming_detection (zc_v2.py:300-346) fused with
+ * detect_zc_peaks (:374-446).  corr_mag: [B][n] f64.  Outputs [B][n], each nullable:
+ * local_sum, corr_scaled, thresh_scaled (f64), above_threshold, metric_valid, gate_mask (u8).
+ * n_events [B] int32 (total, may exceed max_events); ev_int [B][max_events][4] int64 =
+ * peak_index, gate_start, gate_end, detected_start; ev_peak [B][max_events] f64 peak_value.
+ * The running sum is the reference's sequential float64 recursion (bit-identical).
+ */
+int32_t ofs_zc_detect(const double* corr_mag, int64_t B, int64_t n, int32_t window_size,
+                      int64_t thresh_value, int32_t thresh_frac_bits, double min_corr_mag,
+                      int32_t reference_length, int32_t hysteresis, double* local_sum,
+                      double* corr_scaled, double* thresh_scaled, uint8_t* above_threshold,
+                      uint8_t* metric_valid, uint8_t* gate_mask, int32_t max_events,
+                      int32_t* n_events, int64_t* ev_int, double* ev_peak, void* stream);
+
+/* Gate alone on caller-provided flags: replaces zc_v2.detect_zc_peaks (zc_v2.py:374-446). */
+int32_t ofs_zc_gate(const double* corr_mag, const uint8_t* above_threshold, const uint8_t* metric_valid,
+                    int64_t B, int64_t n, int32_t reference_length, int32_t hysteresis,
+                    uint8_t* gate_mask, int32_t max_events, int32_t* n_events, int64_t* ev_int,
+                    double* ev_peak, void* stream);
 
 #ifdef __cplusplus
 }

@@ -187,7 +187,10 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                 if (nb + 2 * j < T) {
                     if (Pout) *reinterpret_cast<float4*>(Pout + 2 * (o + 2 * j)) =
                         make_float4(pf[2 * j][0], pf[2 * j][1], pf[2 * j + 1][0], pf[2 * j + 1][1]);
-                    if constexpr (E % 4 != 0) {
+                    // float4 R/M stores need T % 4 == 0: otherwise the last pair of a stream
+                    // would spill into the next stream's first samples (and b*T+nb is not
+                    // 16-byte aligned for odd b)
+                    if (E % 4 != 0 || (T & 3) != 0) {
                         if (Rout) *reinterpret_cast<float2*>(Rout + o + 2 * j) = make_float2(rf[2 * j], rf[2 * j + 1]);
                         if (Mout) *reinterpret_cast<float2*>(Mout + o + 2 * j) = make_float2(mf[2 * j], mf[2 * j + 1]);
                     } else if ((j & 1) == 0) {

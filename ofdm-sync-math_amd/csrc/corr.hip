@@ -1,0 +1,645 @@
+// corr.hip — the correlation-shaped metrics of the reference on gfx950:
+//   park.park_streaming_metric        (park.py:64-114)      mirror product  Σ x[d-k]·x[d+k]
+//   zc_v2 / zc matched filter         (zc_v2.py:244-271, zc.py:106-126)  Σ x[n-N+1+j]·conj(ref[j])
+//   zc_freq.compute_frequency_metric  (zc_freq.py:62-99)    62-bin sliding DFT per offset
+//   zc_v2 CFAR + gate                 (zc_v2.py:300-446)    sequential FSM, one wave per stream
+//
+// Park and the matched filter are O(T·N) direct sums (no prefix-sum form exists for a
+// mirror product or a correlation against an arbitrary reference).  Both are fp64/fp32
+// vector-FMA bound, not HBM bound: a workgroup stages its input tile (+ halo) in LDS once,
+// every thread then owns OPT consecutive outputs and keeps the OPT-wide sliding window of
+// the input in registers (one LDS load per step feeds OPT complex MACs).  The LDS tile is
+// stored "phase-split" (element j at (j % OPT)·S + j / OPT) so that the per-step loads of
+// a wave (addresses OPT·t + c) hit consecutive LDS words: conflict-free.
+//
+// zc_freq evaluates the 62 template bins of the N-point DFT of every window as a sliding
+// DFT: lane = bin, W_k(s) = Σ_{j=s}^{s+N-1} x[j]·w_k^j is updated by (x[s+N]-x[s])·w_k^s
+// per offset (w_k^{k(s+N)} = w_k^{ks}), with the twiddle w_k^s advanced by one complex
+// multiply and re-anchored exactly (sincospi of an exact integer ratio) every 64 offsets.
+// X_s[k] = conj(w_k^s)·W_k(s), so vdot(t, X_s) = Σ_k conj(t_k·w_k^s)·W_k(s).  The per-offset
+// 62-lane sums are quad-reduced with DPP and finished through a 64-offset LDS transpose,
+// so each lane ends up owning one offset and stores are coalesced.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <algorithm>
+#include "ofdmsync.h"
+#include "ofs_common.h"
+
+namespace {
+
+template <class R> struct C2;
+template <> struct C2<float> { using T = float2; };
+template <> struct C2<double> { using T = double2; };
+
+template <int FMT, class R>
+__device__ __forceinline__ typename C2<R>::T ld_c(const void* p, int64_t i) {
+    typename C2<R>::T o;
+    if constexpr (FMT == OFS_C64) {
+        const float2 v = reinterpret_cast<const float2*>(p)[i];
+        o.x = (R)v.x; o.y = (R)v.y;
+    } else if constexpr (FMT == OFS_C128) {
+        const double2 v = reinterpret_cast<const double2*>(p)[i];
+        o.x = (R)v.x; o.y = (R)v.y;
+    } else {
+        const short2 v = reinterpret_cast<const short2*>(p)[i];
+        o.x = (R)v.x; o.y = (R)v.y;
+    }
+    return o;
+}
+
+constexpr int CW = 256;          // threads per workgroup (Park, matched filter)
+constexpr int OPT = 8;           // consecutive outputs per thread
+constexpr int CD = CW * OPT;     // outputs per workgroup tile
+constexpr int PADF = OPT;        // front pad of the staged tile (Park's backward window)
+
+__host__ __device__ constexpr int64_t split_stride(int64_t len) { return (len + OPT - 1) / OPT | 1; }
+
+// ------------------------------------------------------------------------------------------
+// Park: P(d) = Σ_br Σ_{k<half} x[d-k]·x[d+k]; E(d) = Σ_br Σ_{k<half} |x[d+k]|²;
+//       M = |P|²/max(E,1e-12)²;  d = half + i, i in [0, nout)   (park.py:76-113)
+// Tile: global g in [g0, g0 + len), g0 = d0 - half + 1 - PADF, zero outside [0, T).
+// Thread t, output q: backward b_q = x[d-k], forward f_q = x[d+k]; per step k one new
+// backward value (q = 0) and one new forward value (q = OPT-1) come from LDS; the others
+// rotate through a ring whose slot is (q ∓ k) mod OPT, resolved at compile time by
+// unrolling k by OPT.
+// ------------------------------------------------------------------------------------------
+template <int FMT, class R>
+__global__ __launch_bounds__(CW) void park_kernel(const void* x, int64_t T, int nb, int half,
+                                                  int64_t nout, R* __restrict__ Mo,
+                                                  R* __restrict__ Po, R* __restrict__ Eo) {
+    using V = typename C2<R>::T;
+    extern __shared__ __align__(16) unsigned char smem_raw[];
+    V* seg = reinterpret_cast<V*>(smem_raw);
+    const int t = threadIdx.x;
+    const int64_t b = blockIdx.y;
+    const int64_t i0 = (int64_t)blockIdx.x * CD;
+    const int64_t d0 = half + i0;
+    const int64_t g0 = d0 - half + 1 - PADF;
+    const int64_t len = CD + 2 * (int64_t)half - 2 + 2 * PADF;
+    const int64_t S = split_stride(len);
+    const int ksteps = (half + OPT - 1) / OPT * OPT;
+
+    R pr[OPT], pi[OPT], en[OPT];
+#pragma unroll
+    for (int q = 0; q < OPT; ++q) { pr[q] = 0; pi[q] = 0; en[q] = 0; }
+
+    for (int br = 0; br < nb; ++br) {
+        const int64_t base = (b * nb + br) * T;
+        __syncthreads();
+        for (int64_t j = t; j < len; j += CW) {
+            const int64_t g = g0 + j;
+            V v; v.x = 0; v.y = 0;
+            if (g >= 0 && g < T) v = ld_c<FMT, R>(x, base + g);
+            seg[(j % OPT) * S + j / OPT] = v;
+        }
+        __syncthreads();
+        // seg index of x[d0 + OPT*t + q + m] is PADF + half - 1 + OPT*t + q + m
+        auto at = [&](int64_t j) -> V { return seg[(j % OPT) * S + j / OPT]; };
+        const int64_t c0 = PADF + half - 1 + (int64_t)OPT * t;
+        V bw[OPT], fw[OPT];
+#pragma unroll
+        for (int q = 0; q < OPT; ++q) { bw[q] = at(c0 + q); fw[q] = at(c0 + q); }
+        for (int kk = 0; kk < ksteps; kk += OPT) {
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int k = kk + u;
+                if (k < half) {
+#pragma unroll
+                    for (int q = 0; q < OPT; ++q) {
+                        const V bq = bw[(q - u + OPT) % OPT];
+                        const V fq = fw[(q + u) % OPT];
+                        pr[q] = fma(bq.x, fq.x, fma(-bq.y, fq.y, pr[q]));
+                        pi[q] = fma(bq.x, fq.y, fma(bq.y, fq.x, pi[q]));
+                        en[q] = fma(fq.x, fq.x, fma(fq.y, fq.y, en[q]));
+                    }
+                }
+                // next step: new backward x[d0+OPT t-(k+1)] into slot of b_{OPT-1},
+                //            new forward  x[d0+OPT t+OPT-1+k+1] into slot of f_0
+                bw[(OPT - 1 - u + OPT) % OPT] = at(c0 - (k + 1));
+                fw[u % OPT] = at(c0 + OPT + k);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < OPT; ++q) {
+        const int64_t i = i0 + (int64_t)OPT * t + q;
+        if (i < nout) {
+            const int64_t o = b * nout + i;
+            const R e = en[q] > (R)1e-12 ? en[q] : (R)1e-12;
+            if (Mo) Mo[o] = (pr[q] * pr[q] + pi[q] * pi[q]) / (e * e);
+            if (Po) { Po[2 * o] = pr[q]; Po[2 * o + 1] = pi[q]; }
+            if (Eo) Eo[o] = en[q];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// ZC matched filter (np.convolve(x, conj(ref[::-1]), 'full'), zc_v2.py:244-254):
+//   corr[n] = Σ_{j<N} xz[n-N+1+j]·conj(ref[j]),  n in [0, T+N-1)
+//   energy window (np.convolve(|x|², ones(N)), zc_v2.py:266-268): same window, Σ |xz|²
+// mode 0: raw per branch -> out [B*nb][nout]
+// mode 1: zc_v2 detect_zc_preamble combine (zc_v2.py:493-500): Σ_br corr_br /
+//         (|ref|·sqrt(max(E_br, 1e-12)))
+// mode 2: zc.py:113-126 combine: Σ_br corr_br / (|ref|·sqrt(max(Σ_br E_br, 0) + 1e-12))
+// mode 3: normalize_correlation(corr_in, x, ref) for one branch (zc_v2.py:257-271)
+// mode 4: Σ_br corr_br, un-normalised (detect_zc_preamble with normalize=False, zc_v2.py:493-500)
+// ------------------------------------------------------------------------------------------
+struct ZcArgs {
+    const void* x; int64_t T; int nb; int N; int64_t nout; int mode;
+    const double2* ref; double ref_norm;
+    const double2* corr_in; double2* out; double* mag;
+};
+
+template <int FMT>
+__global__ __launch_bounds__(CW) void zc_mf_kernel(ZcArgs a) {
+    using V = double2;
+    extern __shared__ __align__(16) unsigned char smem_raw[];
+    V* seg = reinterpret_cast<V*>(smem_raw);
+    const int t = threadIdx.x;
+    const int64_t by = blockIdx.y;                   // stream (modes 1-3) or stream*nb+br (mode 0)
+    const int64_t n0 = (int64_t)blockIdx.x * CD;
+    const int N = a.N;
+    const int64_t g0 = n0 - N + 1;
+    const int64_t len = CD + (int64_t)N - 1 + OPT;
+    const int64_t S = split_stride(len);
+    const int jsteps = (N + OPT - 1) / OPT * OPT;
+    const int nbl = (a.mode == 0 || a.mode == 3) ? 1 : a.nb;
+    const bool want_corr = a.mode != 3;
+
+    double sr[OPT], si[OPT], se[OPT];
+#pragma unroll
+    for (int q = 0; q < OPT; ++q) { sr[q] = 0; si[q] = 0; se[q] = 0; }
+
+    for (int br = 0; br < nbl; ++br) {
+        const int64_t row = (a.mode == 0 || a.mode == 3) ? by : by * a.nb + br;
+        const int64_t base = row * a.T;
+        __syncthreads();
+        for (int64_t j = t; j < len; j += CW) {
+            const int64_t g = g0 + j;
+            V v; v.x = 0; v.y = 0;
+            if (g >= 0 && g < a.T) v = ld_c<FMT, double>(a.x, base + g);
+            seg[(j % OPT) * S + j / OPT] = v;
+        }
+        __syncthreads();
+        auto at = [&](int64_t j) -> V { return seg[(j % OPT) * S + j / OPT]; };
+        const int64_t c0 = (int64_t)OPT * t;          // seg index of xz[n0 + OPT t - N + 1]
+        double cr[OPT], ci[OPT], ce[OPT];
+        V fw[OPT];
+#pragma unroll
+        for (int q = 0; q < OPT; ++q) { cr[q] = 0; ci[q] = 0; ce[q] = 0; fw[q] = at(c0 + q); }
+        for (int jj = 0; jj < jsteps; jj += OPT) {
+#pragma unroll
+            for (int u = 0; u < OPT; ++u) {
+                const int j = jj + u;
+                if (j < N) {
+                    const V r = a.ref[j];
+#pragma unroll
+                    for (int q = 0; q < OPT; ++q) {
+                        const V f = fw[(q + u) % OPT];
+                        if (want_corr) {                   // f * conj(r)
+                            cr[q] = fma(f.x, r.x, fma(f.y, r.y, cr[q]));
+                            ci[q] = fma(f.y, r.x, fma(-f.x, r.y, ci[q]));
+                        }
+                        ce[q] = fma(f.x, f.x, fma(f.y, f.y, ce[q]));
+                    }
+                }
+                fw[u % OPT] = at(c0 + OPT + j);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < OPT; ++q) {
+            if (a.mode == 1) {
+                const double d = a.ref_norm * sqrt(ce[q] > 1e-12 ? ce[q] : 1e-12);
+                sr[q] += cr[q] / d; si[q] += ci[q] / d;
+            } else {
+                sr[q] += cr[q]; si[q] += ci[q]; se[q] += ce[q];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < OPT; ++q) {
+        const int64_t n = n0 + (int64_t)OPT * t + q;
+        if (n >= a.nout) continue;
+        const int64_t o = by * a.nout + n;
+        double rr = sr[q], ri = si[q];
+        if (a.mode == 2) {
+            const double d = a.ref_norm * sqrt((se[q] > 0.0 ? se[q] : 0.0) + 1e-12);
+            rr /= d; ri /= d;
+        } else if (a.mode == 3) {
+            const double d = a.ref_norm * sqrt(se[q] > 1e-12 ? se[q] : 1e-12);
+            const V c = a.corr_in[o];
+            rr = c.x / d; ri = c.y / d;
+        }
+        if (a.out) { V v; v.x = rr; v.y = ri; a.out[o] = v; }
+        if (a.mag) a.mag[o] = hypot(rr, ri);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// zc_freq sliding DFT.  One wave per (stream, chunk of offsets); lane = template bin.
+// NB (branches, summed) is a template parameter so the per-branch window sums stay in
+// registers.  fp64 throughout (the metric is a ratio of 62-bin sums).
+// ------------------------------------------------------------------------------------------
+constexpr int ZF_WAVES = 2;
+constexpr int ZF_G = 64;          // offsets per transpose group
+struct ZfArgs {
+    const void* x; int64_t B, T; int N, cp; int64_t noff, chunk, nchunks;
+    int nbins; double t_energy; double* metric;
+    int kb[64]; double tr[64], ti[64];
+};
+
+__device__ __forceinline__ double quad_sum(double v) {
+    v += ofs::dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += ofs::dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+    return v;
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// exp(-2*pi*i*m/N) for an exact integer m in [0, N)
+__device__ __forceinline__ double2 twiddle(int64_t m, int N) {
+    double s, c;
+    sincospi(-2.0 * (double)m / (double)N, &s, &c);
+    return make_double2(c, s);
+}
+
+template <int FMT, int NB>
+__global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
+    __shared__ double red[ZF_WAVES][3][ZF_G][17];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t item = (int64_t)blockIdx.x * ZF_WAVES + wave;
+    if (item >= a.B * a.nchunks) return;              // whole wave; no block barriers below
+    const int64_t b = item / a.nchunks;
+    const int64_t o0 = (item - b * a.nchunks) * a.chunk;
+    const int64_t o1 = min(o0 + a.chunk, a.noff);
+    const int N = a.N;
+    const bool bin_live = lane < a.nbins;
+    const int kb = bin_live ? a.kb[lane] : 0;
+    const double tr = bin_live ? a.tr[lane] : 0.0, ti = bin_live ? a.ti[lane] : 0.0;
+    const double emask = bin_live ? 1.0 : 0.0;
+    const double2 wk = twiddle(kb, N);
+
+    double Wr[NB], Wi[NB];
+#pragma unroll
+    for (int r = 0; r < NB; ++r) { Wr[r] = 0.0; Wi[r] = 0.0; }
+
+    // ---- initial window W_k(s0) = Σ_{j=s0}^{s0+N-1} x[j] w^{kj}
+    const int64_t s0 = o0 + a.cp;
+    for (int64_t j0 = s0; j0 < s0 + N; j0 += 64) {
+        const int cnt = (int)min((int64_t)64, s0 + N - j0);
+        double xr[NB], xi[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            double2 v = make_double2(0.0, 0.0);
+            if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
+            xr[r] = v.x; xi[r] = v.y;
+        }
+        double2 tw = twiddle(((int64_t)kb * j0) % N, N);
+        for (int u = 0; u < cnt; ++u) {
+#pragma unroll
+            for (int r = 0; r < NB; ++r) {
+                const double ur = ofs::readlane(xr[r], u), ui = ofs::readlane(xi[r], u);
+                Wr[r] = fma(ur, tw.x, fma(-ui, tw.y, Wr[r]));
+                Wi[r] = fma(ur, tw.y, fma(ui, tw.x, Wi[r]));
+            }
+            const double nr = tw.x * wk.x - tw.y * wk.y;
+            const double ni = tw.x * wk.y + tw.y * wk.x;
+            tw.x = nr; tw.y = ni;
+        }
+    }
+
+    // ---- slide over the chunk, 64 offsets per transpose group
+    for (int64_t og = o0; og < o1; og += ZF_G) {
+        const int cnt = (int)min((int64_t)ZF_G, o1 - og);
+        const int64_t sg = og + a.cp;
+        double ar[NB], ai[NB], br_[NB], bi[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            const int64_t row = (b * NB + r) * a.T;
+            double2 va = make_double2(0.0, 0.0), vb = make_double2(0.0, 0.0);
+            if (lane < cnt) va = ld_c<FMT, double>(a.x, row + sg + lane);
+            if (lane < cnt && sg + N + lane < a.T) vb = ld_c<FMT, double>(a.x, row + sg + N + lane);
+            ar[r] = va.x; ai[r] = va.y; br_[r] = vb.x; bi[r] = vb.y;
+        }
+        double2 tw = twiddle(((int64_t)kb * sg) % N, N);
+        for (int u = 0; u < cnt; ++u) {
+            double sr = 0.0, si = 0.0, e = 0.0;
+#pragma unroll
+            for (int r = 0; r < NB; ++r) {
+                sr += Wr[r]; si += Wi[r];
+                e = fma(Wr[r], Wr[r], fma(Wi[r], Wi[r], e));
+            }
+            const double ttr = tr * tw.x - ti * tw.y;      // t_k * w^{ks}
+            const double tti = tr * tw.y + ti * tw.x;
+            double cr = ttr * sr + tti * si;              // conj(t w^{ks}) * Σ W
+            double ci = ttr * si - tti * sr;
+            e *= emask;
+            cr = quad_sum(cr); ci = quad_sum(ci); e = quad_sum(e);
+            if ((lane & 3) == 0) {
+                red[wave][0][u][lane >> 2] = cr;
+                red[wave][1][u][lane >> 2] = ci;
+                red[wave][2][u][lane >> 2] = e;
+            }
+#pragma unroll
+            for (int r = 0; r < NB; ++r) {                // W(s+1) = W(s) + (x[s+N]-x[s]) w^{ks}
+                const double dr = ofs::readlane(br_[r], u) - ofs::readlane(ar[r], u);
+                const double di = ofs::readlane(bi[r], u) - ofs::readlane(ai[r], u);
+                Wr[r] = fma(dr, tw.x, fma(-di, tw.y, Wr[r]));
+                Wi[r] = fma(dr, tw.y, fma(di, tw.x, Wi[r]));
+            }
+            const double nr = tw.x * wk.x - tw.y * wk.y;
+            const double ni = tw.x * wk.y + tw.y * wk.x;
+            tw.x = nr; tw.y = ni;
+        }
+        wave_sync();
+        if (lane < cnt) {
+            double Cr = 0.0, Ci = 0.0, E = 0.0;
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                Cr += red[wave][0][lane][g];
+                Ci += red[wave][1][lane][g];
+                E += red[wave][2][lane][g];
+            }
+            const double den = a.t_energy * E;
+            a.metric[b * a.noff + og + lane] = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
+        }
+        wave_sync();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// zc_v2 CFAR + gate (zc_v2.py:300-446), one wave per stream, sequential in sample order
+// (the running sum is the reference's exact left-to-right float64 recursion, so given the
+// same corr_mag the flags and local sums are bit-identical).  gate_only: use caller's
+// above/valid arrays (detect_zc_peaks on an existing state).
+// ------------------------------------------------------------------------------------------
+struct ZdArgs {
+    const double* mag; const uint8_t* above_in; const uint8_t* valid_in;
+    int64_t n; int W; double tv, scale, minmag; int reflen, hyst;
+    double* local_sum; double* corr_scaled; double* thresh_scaled;
+    uint8_t* above; uint8_t* valid; uint8_t* gate_mask;
+    int max_ev; int32_t* n_ev; int64_t* ev; double* ev_v;
+};
+
+__global__ __launch_bounds__(64) void zc_detect_kernel(ZdArgs a) {
+#pragma clang fp contract(off)
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t n = a.n;
+    const double* c = a.mag + b * n;
+    const bool gate_only = a.above_in != nullptr;
+    double acc = 0.0;
+    bool open = false;
+    int64_t gs = 0, pk = 0;
+    double pv = 0.0;
+    int low = 0, nev = 0;
+    const int hl = a.hyst > 1 ? a.hyst - 1 : 0;
+    int64_t* ev = a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr;
+    double* evv = a.ev_v ? a.ev_v + b * (int64_t)a.max_ev : nullptr;
+    for (int64_t base = 0; base < n; base += 64) {
+        const int64_t i = base + lane;
+        const bool inb = i < n;
+        const double ci = inb ? c[i] : 0.0;
+        const double cold = (inb && i >= a.W) ? c[i - a.W] : 0.0;
+        int abl = 0, vdl = 0;
+        if (gate_only) {
+            abl = inb ? (int)a.above_in[b * n + i] : 0;
+            vdl = inb ? (int)a.valid_in[b * n + i] : 0;
+        }
+        const unsigned long long abm = __ballot(abl != 0), vdm = __ballot(vdl != 0);
+        double my_acc = 0.0;
+        int my_mask = 0, my_abv = 0;
+        const int cnt = (int)min((int64_t)64, n - base);
+        for (int u = 0; u < cnt; ++u) {
+            const int64_t idx = base + u;
+            const double cu = ofs::readlane(ci, u);
+            bool vd, abv;
+            if (gate_only) {
+                vd = (vdm >> u) & 1ull;
+                abv = (abm >> u) & 1ull;
+            } else {
+                if (idx >= a.W) acc = (acc + cu) - ofs::readlane(cold, u);
+                else acc = acc + cu;
+                vd = idx >= a.W;
+                abv = vd && (cu * a.scale >= acc * a.tv) && (cu >= a.minmag);
+            }
+            if (lane == u) { my_acc = acc; my_abv = abv; my_mask = vd && open; }
+            if (!vd) continue;
+            if (!open) {
+                if (abv) { open = true; gs = idx; pk = idx; pv = cu; low = 0; }
+            } else {
+                if (cu > pv) { pv = cu; pk = idx; }
+                if (abv) {
+                    low = 0;
+                } else if (a.hyst == 0 || low >= hl) {
+                    if (lane == 0 && ev && nev < a.max_ev) {
+                        int64_t* r = ev + (int64_t)nev * 4;
+                        r[0] = pk; r[1] = gs; r[2] = idx; r[3] = pk - a.reflen + 1 > 0 ? pk - a.reflen + 1 : 0;
+                        if (evv) evv[nev] = pv;
+                    }
+                    ++nev;
+                    open = false; pv = 0.0; low = 0;
+                } else {
+                    ++low;
+                }
+            }
+        }
+        if (inb) {
+            const int64_t o = b * n + i;
+            if (!gate_only) {
+                if (a.local_sum) a.local_sum[o] = my_acc;
+                if (a.corr_scaled) a.corr_scaled[o] = ci * a.scale;
+                if (a.thresh_scaled) a.thresh_scaled[o] = my_acc * a.tv;
+                if (a.above) a.above[o] = (uint8_t)my_abv;
+                if (a.valid) a.valid[o] = (uint8_t)(i >= a.W);
+            }
+            if (a.gate_mask) a.gate_mask[o] = (uint8_t)my_mask;
+        }
+    }
+    if (lane == 0) {
+        if (open) {
+            if (ev && nev < a.max_ev) {
+                int64_t* r = ev + (int64_t)nev * 4;
+                r[0] = pk; r[1] = gs; r[2] = n; r[3] = pk - a.reflen + 1 > 0 ? pk - a.reflen + 1 : 0;
+                if (evv) evv[nev] = pv;
+            }
+            ++nev;
+            if (a.gate_mask) a.gate_mask[b * n + gs] = 1;   // gate_mask[gate_start:n] (rest already set)
+        }
+        if (a.n_ev) a.n_ev[b] = nev;
+    }
+}
+
+static bool fmt_ok(int f) { return f == OFS_C64 || f == OFS_C128 || f == OFS_CI16; }
+
+template <class K>
+static int set_lds(K k, size_t bytes) {
+    if (bytes > 160 * 1024) return OFS_ETOOLONG;
+    if (bytes > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+        return OFS_EHIP;
+    return OFS_OK;
+}
+
+template <int FMT, class R>
+static int park_launch(const void* x, int64_t B, int nb, int64_t T, int half, int64_t nout,
+                       void* M, void* P, void* E, hipStream_t st) {
+    const int64_t len = CD + 2 * (int64_t)half - 2 + 2 * PADF;
+    const size_t lds = (size_t)split_stride(len) * OPT * sizeof(typename C2<R>::T);
+    auto k = park_kernel<FMT, R>;
+    const int rc = set_lds(k, lds);
+    if (rc) return rc;
+    const dim3 grid((unsigned)((nout + CD - 1) / CD), (unsigned)B);
+    hipLaunchKernelGGL(k, grid, dim3(CW), lds, st, x, T, nb, half, nout, (R*)M, (R*)P, (R*)E);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+template <int FMT>
+static int zc_launch(const ZcArgs& a, int64_t rows, hipStream_t st) {
+    const int64_t len = CD + (int64_t)a.N - 1 + OPT;
+    const size_t lds = (size_t)split_stride(len) * OPT * sizeof(double2);
+    auto k = zc_mf_kernel<FMT>;
+    const int rc = set_lds(k, lds);
+    if (rc) return rc;
+    const dim3 grid((unsigned)((a.nout + CD - 1) / CD), (unsigned)rows);
+    hipLaunchKernelGGL(k, grid, dim3(CW), lds, st, a);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+template <int FMT>
+static int zf_launch(const ZfArgs& a, int nb, hipStream_t st) {
+    const int64_t items = a.B * a.nchunks;
+    const dim3 grid((unsigned)((items + ZF_WAVES - 1) / ZF_WAVES));
+    switch (nb) {
+        case 1: hipLaunchKernelGGL((zc_freq_kernel<FMT, 1>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((zc_freq_kernel<FMT, 2>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((zc_freq_kernel<FMT, 3>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        default: hipLaunchKernelGGL((zc_freq_kernel<FMT, 4>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+    }
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ofs_park_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                        int32_t N, int32_t precision, void* M, void* P, void* E, void* stream) {
+    if (!fmt_ok(in_fmt) || !(precision == OFS_FP32 || precision == OFS_FP64) || !x || B < 0 ||
+        n_br < 1 || T < 0 || N < 0)
+        return OFS_EINVAL;
+    const int half = N / 2;
+    if (half == 0 || T < 2 * (int64_t)half + 1 || B == 0) return OFS_OK;   // empty (park.py:79-85)
+    const int64_t nout = T - 2 * (int64_t)half;
+    if (B > 65535) return OFS_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (precision == OFS_FP64) {
+        switch (in_fmt) {
+            case OFS_C64: return park_launch<OFS_C64, double>(x, B, n_br, T, half, nout, M, P, E, st);
+            case OFS_C128: return park_launch<OFS_C128, double>(x, B, n_br, T, half, nout, M, P, E, st);
+            default: return park_launch<OFS_CI16, double>(x, B, n_br, T, half, nout, M, P, E, st);
+        }
+    }
+    switch (in_fmt) {
+        case OFS_C64: return park_launch<OFS_C64, float>(x, B, n_br, T, half, nout, M, P, E, st);
+        case OFS_C128: return park_launch<OFS_C128, float>(x, B, n_br, T, half, nout, M, P, E, st);
+        default: return park_launch<OFS_CI16, float>(x, B, n_br, T, half, nout, M, P, E, st);
+    }
+}
+
+int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                         const void* ref, int32_t N, double ref_energy, int32_t mode,
+                         const void* corr_in, void* corr, double* corr_mag, void* stream) {
+    if (!fmt_ok(in_fmt) || !x || !ref || B < 0 || n_br < 1 || T < 1 || N < 1 || mode < 0 ||
+        mode > 4 || (!corr && !corr_mag) || (mode == 3 && (!corr_in || n_br != 1)) || ref_energy < 0)
+        return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    ZcArgs a;
+    a.x = x; a.T = T; a.nb = n_br; a.N = N; a.nout = T + N - 1; a.mode = mode;
+    a.ref = (const double2*)ref; a.ref_norm = sqrt(ref_energy);
+    a.corr_in = (const double2*)corr_in; a.out = (double2*)corr; a.mag = corr_mag;
+    const int64_t rows = mode == 0 ? B * n_br : B;
+    if (rows > 65535) return OFS_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    switch (in_fmt) {
+        case OFS_C64: return zc_launch<OFS_C64>(a, rows, st);
+        case OFS_C128: return zc_launch<OFS_C128>(a, rows, st);
+        default: return zc_launch<OFS_CI16>(a, rows, st);
+    }
+}
+
+int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                           int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
+                           const double* template_bins, double template_energy, double* metric,
+                           void* stream) {
+    if (!fmt_ok(in_fmt) || !x || !metric || !bin_indices || !template_bins || B < 0 || n_br < 1 ||
+        n_br > 4 || T < 0 || N < 1 || cp < 0 || n_bins < 1 || n_bins > 64)
+        return OFS_EINVAL;
+    const int64_t noff = T - ((int64_t)N + cp) + 1;
+    if (noff <= 0) return OFS_ESHORT;                      // zc_freq.py:76-78 raises
+    if (B == 0) return OFS_OK;
+    ZfArgs a;
+    a.x = x; a.B = B; a.T = T; a.N = N; a.cp = cp; a.noff = noff;
+    a.nbins = n_bins; a.t_energy = template_energy; a.metric = metric;
+    for (int i = 0; i < 64; ++i) {
+        if (i < n_bins) {
+            a.kb[i] = (int)(((bin_indices[i] % N) + N) % N);   // fftshift(fft)[(N/2+k)%N] = fft[k mod N]
+            a.tr[i] = template_bins[2 * i]; a.ti[i] = template_bins[2 * i + 1];
+        } else {
+            a.kb[i] = 0; a.tr[i] = 0.0; a.ti[i] = 0.0;
+        }
+    }
+    int64_t chunk = ((std::max<int64_t>(N, 256) + 63) / 64) * 64;
+    while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < 4096) chunk = ((chunk / 2 + 63) / 64) * 64;
+    a.chunk = chunk;
+    a.nchunks = (noff + chunk - 1) / chunk;
+    hipStream_t st = (hipStream_t)stream;
+    switch (in_fmt) {
+        case OFS_C64: return zf_launch<OFS_C64>(a, n_br, st);
+        case OFS_C128: return zf_launch<OFS_C128>(a, n_br, st);
+        default: return zf_launch<OFS_CI16>(a, n_br, st);
+    }
+}
+
+int32_t ofs_zc_detect(const double* corr_mag, int64_t B, int64_t n, int32_t window_size,
+                      int64_t thresh_value, int32_t thresh_frac_bits, double min_corr_mag,
+                      int32_t reference_length, int32_t hysteresis, double* local_sum,
+                      double* corr_scaled, double* thresh_scaled, uint8_t* above_threshold,
+                      uint8_t* metric_valid, uint8_t* gate_mask, int32_t max_events,
+                      int32_t* n_events, int64_t* ev_int, double* ev_peak, void* stream) {
+    if (!corr_mag || B < 0 || n < 0 || thresh_frac_bits < 0 || thresh_frac_bits > 62 ||
+        max_events < 0 || (max_events > 0 && !ev_int))
+        return OFS_EINVAL;
+    if (B == 0 || n == 0) return OFS_OK;
+    ZdArgs a;
+    a.mag = corr_mag; a.above_in = nullptr; a.valid_in = nullptr;
+    a.n = n; a.W = window_size > 1 ? window_size : 1;          // RunningSum: max(1, W)
+    a.tv = (double)thresh_value; a.scale = (double)(1ll << thresh_frac_bits); a.minmag = min_corr_mag;
+    a.reflen = reference_length; a.hyst = hysteresis;
+    a.local_sum = local_sum; a.corr_scaled = corr_scaled; a.thresh_scaled = thresh_scaled;
+    a.above = above_threshold; a.valid = metric_valid; a.gate_mask = gate_mask;
+    a.max_ev = max_events; a.n_ev = n_events; a.ev = ev_int; a.ev_v = ev_peak;
+    hipLaunchKernelGGL(zc_detect_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_zc_gate(const double* corr_mag, const uint8_t* above_threshold, const uint8_t* metric_valid,
+                    int64_t B, int64_t n, int32_t reference_length, int32_t hysteresis,
+                    uint8_t* gate_mask, int32_t max_events, int32_t* n_events, int64_t* ev_int,
+                    double* ev_peak, void* stream) {
+    if (!corr_mag || !above_threshold || !metric_valid || B < 0 || n < 0 || max_events < 0 ||
+        (max_events > 0 && !ev_int))
+        return OFS_EINVAL;
+    if (B == 0 || n == 0) return OFS_OK;
+    ZdArgs a = {};
+    a.mag = corr_mag; a.above_in = above_threshold; a.valid_in = metric_valid;
+    a.n = n; a.W = 1; a.reflen = reference_length; a.hyst = hysteresis;
+    a.gate_mask = gate_mask; a.max_ev = max_events; a.n_ev = n_events; a.ev = ev_int; a.ev_v = ev_peak;
+    hipLaunchKernelGGL(zc_detect_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, a);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+}  // extern "C"

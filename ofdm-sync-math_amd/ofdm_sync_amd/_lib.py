@@ -42,6 +42,16 @@ def _declare(lib):
                                         P, P]),
         "ofs_cp_cfo": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_int32,
                                  c_double, P, P, P]),
+        "ofs_park_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P,
+                                      P, P]),
+        "ofs_zc_correlate": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_double,
+                                       c_int32, P, P, P, P]),
+        "ofs_zc_freq_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
+                                         c_int32, P, P, c_double, P, P]),
+        "ofs_zc_detect": (c_int32, [P, c_int64, c_int64, c_int32, c_int64, c_int32, c_double, c_int32,
+                                    c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),
+        "ofs_zc_gate": (c_int32, [P, P, P, c_int64, c_int64, c_int32, c_int32, P, c_int32, P, P, P,
+                                  P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -73,7 +83,7 @@ def require_gpu() -> torch.device:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().ofs_status_string(rc).decode()
-        if rc == -1:
+        if rc in (-1, -4):
             raise ValueError(f"{what}: {msg}")
         raise RuntimeError(f"{what}: {msg} (status {rc})")
 

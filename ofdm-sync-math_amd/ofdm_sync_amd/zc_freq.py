@@ -1,0 +1,75 @@
+"""Drop-in for the LTE-style frequency-domain ZC metric of ``zc_freq.py``.
+
+compute_frequency_metric (reference: zc_freq.py:62-99) runs on ``ofs_zc_freq_metric``
+(csrc/corr.hip): the 62 template bins of every window's N-point DFT are produced by a
+sliding DFT (one lane per bin, fp64), not by one FFT per offset.  ``N_FFT`` and
+``CYCLIC_PREFIX`` are read from this module's globals at call time, like the reference.
+The template helpers are host-side setup of 62 constants (zc_freq.py:37-59).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+N_FFT = 2048            # core.py:6
+CYCLIC_PREFIX = 512     # core.py:8
+PSS_LENGTH = 62         # zc_freq.py:30
+PSS_ROOT = 25           # zc_freq.py:31
+
+
+def centered_subcarrier_indices(width: int) -> np.ndarray:
+    """core.py:13-18: +-1 .. +-width/2, skipping DC."""
+    half = width // 2
+    return np.concatenate((np.arange(-half, 0), np.arange(1, half + 1)))
+
+
+def generate_zadoff_chu(root: int, length: int) -> np.ndarray:
+    n = np.arange(length)
+    return np.exp(-1j * np.pi * root * n * (n + 1) / length)
+
+
+def make_pss_frequency_template() -> tuple[np.ndarray, np.ndarray, float]:
+    """Return (centered_bin_indices, template_bins, template_energy) (zc_freq.py:54-59)."""
+    bin_indices = centered_subcarrier_indices(PSS_LENGTH)
+    template_bins = generate_zadoff_chu(PSS_ROOT, PSS_LENGTH)
+    energy = float(np.sum(np.abs(template_bins) ** 2))
+    return bin_indices, template_bins, energy
+
+
+def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, template_energy):
+    idx = np.ascontiguousarray(np.asarray(bin_indices).astype(np.int32))
+    tb = np.ascontiguousarray(np.asarray(template_bins, dtype=np.complex128))
+    if idx.ndim != 1 or tb.shape != idx.shape:
+        raise ValueError("bin_indices and template_bins must be 1-D of equal length")
+    if idx.size > 64 or idx.size == 0:
+        raise ValueError("ofs_zc_freq_metric supports 1..64 template bins")
+    noff = batch.T - (N + cp) + 1
+    if noff <= 0:
+        raise ValueError("Received stream is shorter than a single OFDM symbol.")
+    if batch.nb > 4:
+        raise ValueError("ofs_zc_freq_metric supports up to 4 receive branches")
+    out = torch.empty((batch.B, noff), dtype=torch.float64, device=batch.data.device)
+    rc = _lib.lib().ofs_zc_freq_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T,
+                                       int(N), int(cp), int(idx.size), idx.ctypes.data, tb.ctypes.data,
+                                       float(template_energy), out.data_ptr(), _lib.stream_ptr())
+    _lib.check(rc, "ofs_zc_freq_metric")
+    return out
+
+
+def compute_frequency_metric(rx_samples, bin_indices, template_bins, template_energy: float):
+    """Evaluate the LTE-style frequency-domain metric across all offsets (zc_freq.py:62-99)."""
+    batch = _lib.as_batch(rx_samples, batched=False)
+    out = _run(batch, int(N_FFT), int(CYCLIC_PREFIX), bin_indices, template_bins, template_energy)
+    return _lib.to_host(out[0], np.float64) if batch.from_numpy else out[0]
+
+
+def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, template_energy=None,
+                                     N: int | None = None, cp: int | None = None):
+    """Batched metric over x[B, n_branch, T] -> device tensor [B, T-(N+cp)+1] (f64)."""
+    if bin_indices is None:
+        bin_indices, template_bins, template_energy = make_pss_frequency_template()
+    batch = _lib.as_batch(x, batched=True)
+    return _run(batch, int(N_FFT if N is None else N), int(CYCLIC_PREFIX if cp is None else cp),
+                bin_indices, template_bins, template_energy)

@@ -1,0 +1,248 @@
+"""GPU parity for the correlation-shaped metrics (csrc/corr.hip), through the C ABI:
+Park (park.py:64-114), the ZC frequency-domain metric (zc_freq.py:62-99), the ZC matched
+filter / normaliser / combiner (zc_v2.py:244-271, zc.py:106-126) and the zc_v2 CFAR + gate
+(zc_v2.py:300-446), against the reference goldens and the CPU oracle.
+
+Tolerances (written here):
+  fp64 paths: complex sums within 1e-11 of the stream maximum; normalised metrics within
+      1e-9 relative + 1e-11 absolute (a direct O(N) sum or a sliding DFT in a different
+      summation order than numpy's pocketfft / np.convolve);
+  fp32 Park (complex64 input): P, E within 1e-4 of the stream maximum;
+  CFAR/gate given the same corr_mag: bit-identical (the kernel runs the reference's
+      sequential float64 recursion); end to end, events identical and flags identical
+      except at samples whose threshold margin is below 1e-9 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from ofdm_sync_amd import park, zc_freq, zc_v2, zc  # noqa: E402
+
+
+def G(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    if a.size == 0:
+        return 0.0
+    return float(np.max(np.abs(a - b)) / max(1e-300, float(np.max(np.abs(b)))))
+
+
+def rng_c(rng, *shape):
+    return rng.standard_normal(shape) + 1j * rng.standard_normal(shape)
+
+
+# ------------------------------------------------------------------ Park ---------------
+@pytest.mark.parametrize("name", ["park_N2048", "park_N256", "park_N64"])
+def test_park_vs_reference_golden(name, monkeypatch):
+    d = G(name)
+    monkeypatch.setattr(park, "N_FFT", int(d["N"]))
+    ds, M, P, E = park.park_streaming_metric(d["x"])
+    assert isinstance(M, np.ndarray) and M.dtype == np.float64 and P.dtype == np.complex128
+    assert np.array_equal(ds, d["ds"])
+    assert rel(P, d["P"]) < 1e-11
+    assert rel(E, d["E"]) < 1e-12
+    np.testing.assert_allclose(M, d["M"], rtol=1e-9, atol=1e-11)
+    assert int(np.argmax(M)) == int(np.argmax(d["M"]))
+
+
+@pytest.mark.parametrize("N,T,nb,fmt", [(64, 400, 1, "c128"), (130, 1000, 2, "c128"), (65, 300, 3, "c128"),
+                                        (512, 5000, 2, "i16"), (2048, 4097, 1, "c128"),
+                                        (4096, 9000, 1, "c128"), (16, 17, 1, "c128")])
+def test_park_batched_vs_oracle(N, T, nb, fmt):
+    rng = np.random.default_rng(N + T)
+    B = 3
+    if fmt == "i16":
+        xi = rng.integers(-2048, 2048, size=(B, nb, T, 2)).astype(np.int16)
+        x = xi[..., 0] + 1j * xi[..., 1]
+        ds, M, P, E = park.park_streaming_metric_batched(torch.from_numpy(xi).cuda(), N=N)
+    else:
+        x = rng_c(rng, B, nb, T)
+        ds, M, P, E = park.park_streaming_metric_batched(torch.from_numpy(x).cuda(), N=N)
+    for b in range(B):
+        dso, Mo, Po, Eo = O.park_metric(x[b], N)
+        assert np.array_equal(ds.cpu().numpy(), dso)
+        assert rel(P[b].cpu().numpy(), Po) < 1e-11
+        assert rel(E[b].cpu().numpy(), Eo) < 1e-12
+        np.testing.assert_allclose(M[b].cpu().numpy(), Mo, rtol=1e-9, atol=1e-12)
+        if fmt == "i16":                     # integer input: every partial sum exact
+            assert np.array_equal(P[b].cpu().numpy(), Po) and np.array_equal(E[b].cpu().numpy(), Eo)
+
+
+def test_park_fp32_complex64():
+    rng = np.random.default_rng(5)
+    x = rng_c(rng, 4, 1, 3000).astype(np.complex64)
+    ds, M, P, E = park.park_streaming_metric_batched(torch.from_numpy(x).cuda(), N=512)
+    assert M.dtype == torch.float32
+    for b in range(4):
+        _, Mo, Po, Eo = O.park_metric(x[b].astype(np.complex128), 512)
+        assert rel(P[b].cpu().numpy(), Po) < 1e-4
+        assert rel(E[b].cpu().numpy(), Eo) < 1e-5
+
+
+def test_park_empty_like_reference(monkeypatch):
+    monkeypatch.setattr(park, "N_FFT", 64)
+    ds, M, P, E = park.park_streaming_metric(np.ones(64, complex))      # T < N+1
+    assert ds.size == M.size == P.size == E.size == 0
+    ds, M, P, E = park.park_streaming_metric(np.ones(65, complex))      # exactly one output
+    assert list(ds) == [32] and M.size == 1
+
+
+# ------------------------------------------------------------------ zc_freq ------------
+@pytest.mark.parametrize("name", ["zcfreq_N2048", "zcfreq_N256"])
+def test_zc_freq_vs_reference_golden(name, monkeypatch):
+    d = G(name)
+    monkeypatch.setattr(zc_freq, "N_FFT", int(d["N"]))
+    monkeypatch.setattr(zc_freq, "CYCLIC_PREFIX", int(d["CP"]))
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    assert np.array_equal(idx, d["bins"]) and e == float(d["template_energy"])
+    m = zc_freq.compute_frequency_metric(d["x"], idx, t, e)
+    assert m.dtype == np.float64 and m.shape == d["metric"].shape
+    np.testing.assert_allclose(m, d["metric"], rtol=1e-9, atol=1e-11)
+    assert int(np.argmax(m)) == int(np.argmax(d["metric"]))
+
+
+@pytest.mark.parametrize("N,cp,T,nb", [(256, 64, 2000, 1), (256, 64, 2000, 2), (128, 0, 700, 3),
+                                       (512, 128, 4000, 4), (4096, 1024, 6000, 1), (64, 16, 80, 1)])
+def test_zc_freq_batched_vs_oracle(N, cp, T, nb):
+    rng = np.random.default_rng(N * 7 + nb)
+    B = 3
+    x = rng_c(rng, B, nb, T)
+    # a ZC-bearing symbol in stream 1 so the metric has a real peak
+    idx, t, e = O.zc_template()
+    if T >= 300 + N:
+        x[1, :, 300:300 + N] += 4 * O.pss_symbol(N)
+    m = zc_freq.compute_frequency_metric_batched(torch.from_numpy(x).cuda(), idx, t, e, N=N, cp=cp)
+    for b in range(B):
+        mo = O.zc_freq_metric(x[b], N, cp, idx, t, e)
+        np.testing.assert_allclose(m[b].cpu().numpy(), mo, rtol=1e-9, atol=1e-11)
+
+
+def test_zc_freq_too_short_raises(monkeypatch):
+    monkeypatch.setattr(zc_freq, "N_FFT", 64)
+    monkeypatch.setattr(zc_freq, "CYCLIC_PREFIX", 16)
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    with pytest.raises(ValueError):
+        zc_freq.compute_frequency_metric(np.ones(79, complex), idx, t, e)
+    assert zc_freq.compute_frequency_metric(np.ones(80, complex), idx, t, e).shape == (1,)
+
+
+# ------------------------------------------------------------------ ZC matched filter --
+def test_zc_matched_filter_vs_reference_golden():
+    d = G("zc_mf")
+    x, ref = d["x"], d["ref"]
+    for b in range(x.shape[0]):
+        c = zc_v2.matched_filter_correlation(x[b], ref)
+        assert c.dtype == np.complex128 and c.shape == d["corr"][b].shape
+        assert rel(c, d["corr"][b]) < 1e-11
+        nrm = zc_v2.normalize_correlation(d["corr"][b], x[b], ref)
+        assert rel(nrm, d["norm"][b]) < 1e-11
+    comb = zc.combined_matched_filter(x, d["zc_ref"])
+    assert rel(comb, d["zc_combined"]) < 1e-11
+
+
+def test_zc_detect_preamble_vs_reference_golden():
+    d = G("zc_mf")
+    r = zc_v2.detect_zc_preamble(d["x"])
+    st = r.state
+    np.testing.assert_allclose(st.corr_mag, d["corr_mag"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(st.local_sum, d["local_sum"], rtol=1e-9, atol=1e-9)
+    assert np.array_equal(st.metric_valid, d["metric_valid"])
+    # flags may only differ where the comparison margin is at rounding level
+    diff = st.above_threshold != d["above_threshold"]
+    margin = np.abs(d["corr_scaled"] - d["thresh_scaled"]) / np.maximum(np.abs(d["thresh_scaled"]), 1e-300)
+    margin2 = np.abs(d["corr_mag"] - float(d["min_corr_mag"]))
+    assert np.all((margin[diff] < 1e-9) | (margin2[diff] < 1e-9))
+    ev = np.array([[e.peak_index, e.gate_start, e.gate_end, e.detected_start] for e in r.events]).reshape(-1, 4)
+    assert np.array_equal(ev, d["events"])
+    np.testing.assert_allclose([e.peak_value for e in r.events], d["peak_values"], rtol=1e-9)
+    assert np.array_equal(r.gate_mask, d["gate_mask"])
+
+
+@pytest.mark.parametrize("hyst", [0, 1, 5, 64])
+def test_zc_cfar_and_gate_bit_identical_given_corr_mag(hyst):
+    rng = np.random.default_rng(hyst)
+    B, n, W = 4, 3000, 128
+    mag = np.abs(rng_c(rng, B, n)) * 0.2
+    for b in range(B):
+        for p in rng.integers(W, n - 50, size=6):
+            mag[b, p:p + rng.integers(1, 40)] += rng.uniform(0.5, 3.0)
+    mag[3, n - 5:] += 5.0                              # gate still open at the end
+    mt = torch.from_numpy(mag).cuda()
+    st, gate, n_ev, ev_i, ev_v = zc_v2._detect_run(mt, W, 200, 15, 0.3, 2048, hyst, 4096)
+    for b in range(B):
+        so = O.zc_streaming_detection(mag[b], W, 200, 15, 0.3)
+        for k in ("local_sum", "corr_scaled", "thresh_scaled"):
+            assert np.array_equal(st[k][b].cpu().numpy(), so[k]), k
+        assert np.array_equal(st["above_threshold"][b].cpu().numpy().astype(bool), so["above_threshold"])
+        assert np.array_equal(st["metric_valid"][b].cpu().numpy().astype(bool), so["metric_valid"])
+        evo, valo, masko = O.detect_zc_peaks(mag[b], so["above_threshold"], so["metric_valid"], 2048, hyst)
+        k = int(n_ev[b])
+        assert k == len(evo) and k > 0
+        assert np.array_equal(ev_i[b, :k].cpu().numpy(), evo)
+        assert np.array_equal(ev_v[b, :k].cpu().numpy(), valo)
+        assert np.array_equal(gate[b].cpu().numpy().astype(bool), masko)
+
+
+@pytest.mark.parametrize("hyst", [0, 2, 7])
+def test_zc_gate_on_given_state(hyst):
+    rng = np.random.default_rng(100 + hyst)
+    n = 2500
+    mag = rng.uniform(0, 1, n)
+    above = rng.uniform(0, 1, n) < 0.15
+    valid = rng.uniform(0, 1, n) < 0.9               # not monotonic: exercises the skip
+    st = zc_v2.ZCDetectionState(corr_mag=mag, local_sum=np.zeros(n), corr_scaled=mag, thresh_scaled=mag,
+                                above_threshold=above, metric_valid=valid)
+    r = zc_v2.detect_zc_peaks(st, reference_length=300, hysteresis=hyst)
+    evo, valo, masko = O.detect_zc_peaks(mag, above, valid, 300, hyst)
+    ev = np.array([[e.peak_index, e.gate_start, e.gate_end, e.detected_start] for e in r.events]).reshape(-1, 4)
+    assert len(r.events) > 16                         # exercises the event-buffer regrowth
+    assert np.array_equal(ev, evo)
+    assert np.array_equal([e.peak_value for e in r.events], valo)
+    assert np.array_equal(r.gate_mask, masko)
+
+
+def test_zc_batched_preamble_vs_oracle():
+    rng = np.random.default_rng(77)
+    B, nb, T = 5, 2, 7000
+    ref = O.pss_symbol(2048)
+    x = rng_c(rng, B, nb, T) * 0.3
+    for b in range(B):
+        if b != 2:
+            x[b, :, 1000 + 500 * b:1000 + 500 * b + 2048] += ref
+    r = zc_v2.detect_zc_preamble_batched(torch.from_numpy(x).cuda(), ref)
+    for b in range(B):
+        mag = np.abs(sum(O.normalize_correlation(O.matched_filter(x[b, k], ref), x[b, k], ref)
+                         for k in range(nb)))
+        np.testing.assert_allclose(r.corr_mag[b].cpu().numpy(), mag, rtol=1e-9, atol=1e-12)
+        so = O.zc_streaming_detection(r.corr_mag[b].cpu().numpy(), zc_v2.CORR_WINDOW_SIZE, zc_v2.THRESH_VALUE,
+                                      zc_v2.THRESH_FRAC_BITS, zc_v2.MIN_CORR_MAG)
+        evo, valo, _ = O.detect_zc_peaks(so["corr_mag"], so["above_threshold"], so["metric_valid"], 2048,
+                                         zc_v2.HYSTERESIS)
+        k = int(r.n_events[b])
+        assert np.array_equal(r.events[b, :k].cpu().numpy(), evo)
+        if b != 2:      # the preamble's full-overlap peak is among the detections
+            assert k >= 1 and np.min(np.abs(evo[:, 0] - (1000 + 500 * b + 2047))) <= 2
+
+
+def test_zc_combined_batched_vs_oracle():
+    rng = np.random.default_rng(3)
+    ref = O.pss_symbol(1024)
+    x = rng_c(rng, 3, 2, 3000)
+    corr, mag = zc.combined_matched_filter_batched(torch.from_numpy(x).cuda(), ref)
+    for b in range(3):
+        co = O.zc_combined(x[b], ref)
+        assert rel(corr[b].cpu().numpy(), co) < 1e-11
+        np.testing.assert_allclose(mag[b].cpu().numpy(), np.abs(co), rtol=1e-11, atol=1e-14)
