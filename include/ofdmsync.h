@@ -132,6 +132,25 @@ int32_t ofs_minn_rtl_gate(const double* corr_positive, const uint8_t* above_thre
                           void* stream);
 
 /*
+ * combined_sc_min detector front end (combined_sc_min.py:333-334: minn_streaming_metric and
+ * schmidl_cox_streaming_metric on the same rx): both metrics in one pass over the input
+ * (fused fp32 kernel for complex64 / one branch / N/4 a multiple of 64; otherwise the two
+ * kernels above back to back).  Outputs as ofs_sc_metric (r_mode 1) and ofs_minn_metric.
+ */
+int32_t ofs_sc_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                           int32_t symbol_len, int32_t precision, void* M_sc, void* P_sc, void* R_sc,
+                           void* M_minn, void* P_minn, void* R_minn, void* stream);
+
+/*
+ * Which kernel a window-metric call runs on: kind 1 = ofs_sc_metric r_mode 0, 2 = r_mode 1,
+ * 3 = ofs_minn_metric, 4 = ofs_sc_minn_metric.  Returns 10*E + MW of the streaming fp32 fast kernel (win_fast.hip:
+ * complex64, one branch, even T, window of MW rows of 64*E samples), or 0 for the general
+ * LDS-tiled engine.
+ */
+int32_t ofs_win_plan(int32_t kind, int32_t in_fmt, int32_t precision, int32_t n_br, int64_t T,
+                     int32_t symbol_len);
+
+/*
  * CP-correlation CFO: replaces core.estimate_cfo_from_cp (core.py:179-196), batched with a
  * per-stream CP start.  starts: [B] int64 (device); P_out: [B][2] f64 (nullable);
  * cfo_out: [B] f64.  Windows must lie inside [0, T) (checked by the caller).
@@ -166,17 +185,21 @@ int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
                          const void* corr_in, void* corr, double* corr_mag, void* stream);
 
 /*
- * ZC frequency-domain metric (fp64): replaces zc_freq.compute_frequency_metric
- * (zc_freq.py:62-99).  For off in [0, T-(N+cp)]: 62-bin DFT of x[off+cp : off+cp+N] at
- * fftshift positions (N/2 + bin_indices) % N, metric = |sum_br vdot(t, bins)|^2 /
- * max(E_t * sum_br sum |bins|^2, 1e-12).  bin_indices [n_bins] int32 and template_bins
- * [n_bins] c128 are HOST pointers (n_bins <= 64); metric: [B][T-(N+cp)+1] f64 (device).
- * n_br <= 4.  Returns OFS_ESHORT when T < N + cp (the reference raises ValueError).
+ * ZC frequency-domain metric: replaces zc_freq.compute_frequency_metric (zc_freq.py:62-99).
+ * For off in [0, T-(N+cp)]: 62-bin DFT of x[off+cp : off+cp+N] at fftshift positions
+ * (N/2 + bin_indices) % N, metric = |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum|bins|^2, 1e-12).
+ * bin_indices [n_bins] int32 and template_bins [n_bins] c128 are HOST pointers (n_bins <= 64);
+ * metric: [B][T-(N+cp)+1] (device), f64 for OFS_FP64 (sliding DFT, n_br <= 4), f32 for
+ * OFS_FP32 (per-window 64 x N/64 pruned FFT; needs OFS_C64, N = 64*2^j <= 4096 and at most
+ * 64 offsets per stream: the cfg5 one-window-per-sequence shape).  Returns OFS_ESHORT when
+ * T < N + cp (the reference raises ValueError).
  */
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
-                           int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
-                           const double* template_bins, double template_energy, double* metric,
-                           void* stream);
+                           int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
+                           const int32_t* bin_indices, const double* template_bins,
+                           double template_energy, void* metric, void* stream);
+/* which zc_freq kernel a shape runs on: 1 sliding DFT (fp64), 2 window FFT (fp32), 0 none */
+int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp);
 
 /*
  * ZC CFAR + gate: replaces zc_v2.zc_streaming_detection (zc_v2.py:300-346) fused with

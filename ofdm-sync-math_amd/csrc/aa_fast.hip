@@ -39,23 +39,6 @@ constexpr int FAST_WG = 256;      // 4 waves = 4 independent streams per workgro
 constexpr int TMAX = 1024;        // stream length handled by the fast path
 constexpr int NOKEY = 1 << 20;
 
-// zero-filled DPP move (bound_ctrl): lanes without a source read 0
-template <int CTRL, int RMASK = 0xf>
-__device__ __forceinline__ double dppz(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RMASK, 0xf, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RMASK, 0xf, true);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double scan_add(double v) {
-    v += dppz<0x111>(v);            // row_shr:1
-    v += dppz<0x112>(v);            // row_shr:2
-    v += dppz<0x114>(v);            // row_shr:4
-    v += dppz<0x118>(v);            // row_shr:8
-    v += dppz<0x142, 0xa>(v);       // row_bcast:15 -> rows 1, 3
-    v += dppz<0x143, 0xc>(v);       // row_bcast:31 -> rows 2, 3
-    return v;
-}
-__device__ __forceinline__ double shr1z(double v) { return dppz<0x138>(v); }   // wave_shr:1, lane 0 <- 0
 
 // Stream staging: the wave DMAs its whole stream into a private 8 KiB LDS slice
 // (global_load_lds_dwordx4: no VGPRs, one contiguous 1 KiB per wave-instruction) and reads

@@ -245,7 +245,7 @@ constexpr int ZF_WAVES = 2;
 constexpr int ZF_G = 64;          // offsets per transpose group
 struct ZfArgs {
     const void* x; int64_t B, T; int N, cp; int64_t noff, chunk, nchunks;
-    int nbins; double t_energy; double* metric;
+    int nbins; double t_energy; void* metric;
     int kb[64]; double tr[64], ti[64];
 };
 
@@ -269,7 +269,7 @@ __device__ __forceinline__ double2 twiddle(int64_t m, int N) {
 template <int FMT, int NB>
 __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
     __shared__ double red[ZF_WAVES][3][ZF_G][17];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t item = (int64_t)blockIdx.x * ZF_WAVES + wave;
     if (item >= a.B * a.nchunks) return;              // whole wave; no block barriers below
     const int64_t b = item / a.nchunks;
@@ -364,9 +364,129 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
                 E += red[wave][2][lane][g];
             }
             const double den = a.t_energy * E;
-            a.metric[b * a.noff + og + lane] = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
+            static_cast<double*>(a.metric)[b * a.noff + og + lane] = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
         }
         wave_sync();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// zc_freq, few offsets per stream (cfg5: one window per sequence), fp32: pruned DFT by a
+// 64 x R split.  N = 64 R, n = 64 a + c:  X[k] = Σ_c w_N^{kc} · Y_c[k mod R],
+// Y_c[r] = Σ_a x[64a + c] w_R^{ra}.  Lane c loads column c (each load instruction reads 64
+// consecutive samples: coalesced), runs an R-point radix-2 FFT in registers (twiddles are
+// compile-time constants), and parks Y in LDS [r][c]; lane j then owns template bin k_j and
+// sums its 64 column terms with an fp64 twiddle recurrence.  ~16 K complex MACs per window
+// instead of 62·N for a direct DFT, and one read of the window: HBM-bound at cfg5's size.
+// ------------------------------------------------------------------------------------------
+constexpr double kPi = 3.14159265358979323846;
+constexpr double c_sin(double x) {          // |x| <= pi, Taylor to 1e-17
+    double t = x, s = x;
+    for (int i = 1; i < 30; ++i) { t *= -x * x / ((2 * i) * (2 * i + 1)); s += t; }
+    return s;
+}
+constexpr double c_cos(double x) {
+    double t = 1, s = 1;
+    for (int i = 1; i < 30; ++i) { t *= -x * x / ((2 * i - 1) * (2 * i)); s += t; }
+    return s;
+}
+struct Tw64 {
+    float c[32], s[32];
+    constexpr Tw64() : c(), s() {
+        for (int m = 0; m < 32; ++m) { c[m] = (float)c_cos(2 * kPi * m / 64); s[m] = (float)-c_sin(2 * kPi * m / 64); }
+    }
+};
+constexpr int bitrev(int i, int bits) {
+    int r = 0;
+    for (int b = 0; b < bits; ++b) r |= ((i >> b) & 1) << (bits - 1 - b);
+    return r;
+}
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v >> 1); }
+
+// in-register forward DFT of R points (natural order in, natural order out)
+template <int R>
+__device__ __forceinline__ void fft_reg(float (&re)[R], float (&im)[R]) {
+    constexpr Tw64 TW{};
+    constexpr int LB = ilog2(R);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int j = bitrev(i, LB);
+        if (j > i) {
+            const float tr = re[i], ti = im[i];
+            re[i] = re[j]; im[i] = im[j]; re[j] = tr; im[j] = ti;
+        }
+    }
+#pragma unroll
+    for (int len = 2; len <= R; len <<= 1) {
+#pragma unroll
+        for (int i = 0; i < R; i += len) {
+#pragma unroll
+            for (int k = 0; k < len / 2; ++k) {
+                const int m = k * (64 / len);                    // w_len^k = w_64^m
+                const float wr = TW.c[m], wi = TW.s[m];
+                const int p = i + k, q = i + k + len / 2;
+                const float tr = re[q] * wr - im[q] * wi;
+                const float ti = re[q] * wi + im[q] * wr;
+                re[q] = re[p] - tr; im[q] = im[p] - ti;
+                re[p] = re[p] + tr; im[p] = im[p] + ti;
+            }
+        }
+    }
+}
+
+constexpr int ZW_WAVES = 2;
+template <int R>
+__global__ __launch_bounds__(64 * ZW_WAVES) void zc_win_kernel(ZfArgs a, int nb) {
+    __shared__ float2 Y[ZW_WAVES][R][65];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t item = (int64_t)blockIdx.x * ZW_WAVES + wave;
+    if (item >= a.B * a.noff) return;                      // whole wave
+    const int64_t b = item / a.noff;
+    const int64_t o = item - b * a.noff;
+    const int N = a.N;
+    const bool live = lane < a.nbins;
+    const int kb = live ? a.kb[lane] : 0;
+    const int rj = kb & (R - 1);
+    double s, c;
+    sincospi(-2.0 * (double)kb / (double)N, &s, &c);       // w_N^{k}
+    const double tr = live ? a.tr[lane] : 0.0, ti = live ? a.ti[lane] : 0.0;
+    double cr = 0.0, ci = 0.0, e = 0.0;
+    for (int br = 0; br < nb; ++br) {
+        const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * nb + br) * a.T + o + a.cp;
+        float re[R], im[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float2 v = xs[64 * q + lane];
+            re[q] = v.x; im[q] = v.y;
+        }
+        fft_reg<R>(re, im);
+#pragma unroll
+        for (int r = 0; r < R; ++r) Y[wave][r][lane] = make_float2(re[r], im[r]);
+        wave_sync();
+        double xr = 0.0, xi = 0.0, twr = 1.0, twi = 0.0;
+        asm volatile("" : "+v"(c), "+v"(s));   // keep the recurrence in the loop (no 64-entry hoist)
+        for (int col = 0; col < 64; ++col) {
+            const float2 y = Y[wave][rj][col];
+            xr += twr * y.x - twi * y.y;
+            xi += twr * y.y + twi * y.x;
+            const double nr = twr * c - twi * s;
+            twi = twr * s + twi * c;
+            twr = nr;
+        }
+        wave_sync();
+        cr += tr * xr + ti * xi;                           // conj(t) * X
+        ci += tr * xi - ti * xr;
+        e += live ? xr * xr + xi * xi : 0.0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        cr += __shfl_xor(cr, off, 64);
+        ci += __shfl_xor(ci, off, 64);
+        e += __shfl_xor(e, off, 64);
+    }
+    if (lane == 0) {
+        const double den = a.t_energy * e;
+        static_cast<float*>(a.metric)[item] = (float)((cr * cr + ci * ci) / (den > 1e-12 ? den : 1e-12));
     }
 }
 
@@ -509,6 +629,27 @@ static int zc_launch(const ZcArgs& a, int64_t rows, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
 
+static int zw_launch(const ZfArgs& a, int nb, hipStream_t st) {
+    const int64_t items = a.B * a.noff;
+    const dim3 grid((unsigned)((items + ZW_WAVES - 1) / ZW_WAVES));
+    switch (a.N / 64) {
+        case 2: hipLaunchKernelGGL(zc_win_kernel<2>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+        case 4: hipLaunchKernelGGL(zc_win_kernel<4>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+        case 8: hipLaunchKernelGGL(zc_win_kernel<8>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+        case 16: hipLaunchKernelGGL(zc_win_kernel<16>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+        case 32: hipLaunchKernelGGL(zc_win_kernel<32>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+        default: hipLaunchKernelGGL(zc_win_kernel<64>, grid, dim3(64 * ZW_WAVES), 0, st, a, nb); break;
+    }
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+// the window-FFT kernel serves fp32 calls with few offsets per stream (cfg5 shape)
+static bool zw_ok(int in_fmt, int precision, int N, int64_t noff) {
+    const int R = N / 64;
+    return in_fmt == OFS_C64 && precision == OFS_FP32 && N % 64 == 0 && R >= 2 && R <= 64 &&
+           (R & (R - 1)) == 0 && noff <= 64;
+}
+
 template <int FMT>
 static int zf_launch(const ZfArgs& a, int nb, hipStream_t st) {
     const int64_t items = a.B * a.nchunks;
@@ -572,11 +713,12 @@ int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
 }
 
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
-                           int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
-                           const double* template_bins, double template_energy, double* metric,
-                           void* stream) {
+                           int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
+                           const int32_t* bin_indices, const double* template_bins,
+                           double template_energy, void* metric, void* stream) {
     if (!fmt_ok(in_fmt) || !x || !metric || !bin_indices || !template_bins || B < 0 || n_br < 1 ||
-        n_br > 4 || T < 0 || N < 1 || cp < 0 || n_bins < 1 || n_bins > 64)
+        T < 0 || N < 1 || cp < 0 || n_bins < 1 || n_bins > 64 ||
+        !(precision == OFS_FP32 || precision == OFS_FP64))
         return OFS_EINVAL;
     const int64_t noff = T - ((int64_t)N + cp) + 1;
     if (noff <= 0) return OFS_ESHORT;                      // zc_freq.py:76-78 raises
@@ -592,16 +734,28 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
             a.kb[i] = 0; a.tr[i] = 0.0; a.ti[i] = 0.0;
         }
     }
+    hipStream_t st = (hipStream_t)stream;
+    if (precision == OFS_FP32) {
+        if (!zw_ok(in_fmt, precision, N, noff)) return OFS_EINVAL;
+        return zw_launch(a, n_br, st);
+    }
+    if (n_br > 4) return OFS_EINVAL;
     int64_t chunk = ((std::max<int64_t>(N, 256) + 63) / 64) * 64;
     while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < 4096) chunk = ((chunk / 2 + 63) / 64) * 64;
     a.chunk = chunk;
     a.nchunks = (noff + chunk - 1) / chunk;
-    hipStream_t st = (hipStream_t)stream;
     switch (in_fmt) {
         case OFS_C64: return zf_launch<OFS_C64>(a, n_br, st);
         case OFS_C128: return zf_launch<OFS_C128>(a, n_br, st);
         default: return zf_launch<OFS_CI16>(a, n_br, st);
     }
+}
+
+int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp) {
+    const int64_t noff = T - ((int64_t)N + cp) + 1;
+    if (noff <= 0) return 0;
+    if (precision == OFS_FP32) return zw_ok(in_fmt, precision, N, noff) ? 2 : 0;
+    return 1;
 }
 
 int32_t ofs_zc_detect(const double* corr_mag, int64_t B, int64_t n, int32_t window_size,

@@ -825,10 +825,15 @@ int32_t ofs_sc_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, in
     if (symbol_len < 2 || (symbol_len & 1) || (r_mode != 0 && r_mode != 1)) return OFS_EINVAL;
     const int64_t n_out = T - symbol_len + 1;
     if (B == 0 || n_out <= 0) return OFS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    {
+        const WinFastArgs f{x, B, T, symbol_len, M, P, R};
+        const int frc = ofs_win_fast_try(r_mode == 0 ? 1 : 2, in_fmt, precision, n_br, f, st);
+        if (frc != 0) return frc > 0 ? OFS_OK : frc;
+    }
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = n_out; a.nb = n_br; a.D = symbol_len / 2; a.W = symbol_len / 2;
     a.N = symbol_len; a.P = P; a.R = R; a.M = M;
-    hipStream_t st = (hipStream_t)stream;
     return r_mode == 0 ? dispatch_win<M_SC>(in_fmt, precision, a, B, 0, symbol_len - 1, st, nullptr)
                        : dispatch_win<M_COMB>(in_fmt, precision, a, B, 0, symbol_len - 1, st, nullptr);
 }
@@ -840,6 +845,11 @@ int32_t ofs_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, 
         return OFS_EINVAL;
     const int64_t n_out = T - symbol_len + 1;
     if (B == 0 || n_out <= 0) return OFS_OK;
+    {
+        const WinFastArgs f{x, B, T, symbol_len, M, P, R};
+        const int frc = ofs_win_fast_try(3, in_fmt, precision, n_br, f, (hipStream_t)stream);
+        if (frc != 0) return frc > 0 ? OFS_OK : frc;
+    }
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = n_out; a.nb = n_br; a.Q = symbol_len / 4; a.D = symbol_len / 4;
     a.N = symbol_len; a.P = P; a.R = R; a.M = M;
@@ -896,6 +906,28 @@ int32_t ofs_minn_rtl_gate(const double* corr_positive, const uint8_t* above_thre
                        corr_positive, above_threshold, metric_valid, T, hysteresis, timing_offset,
                        max_events, n_events, events, open_gate_start);
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_sc_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                           int32_t symbol_len, int32_t precision, void* M_sc, void* P_sc, void* R_sc,
+                           void* M_minn, void* P_minn, void* R_minn, void* stream) {
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || !x || B < 0 || n_br < 1 || T < 0 || symbol_len < 2 ||
+        (symbol_len & 1))
+        return OFS_EINVAL;
+    if (B == 0 || T - symbol_len + 1 <= 0) return OFS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int frc = ofs_sc_minn_fast_try(in_fmt, precision, n_br, x, B, T, symbol_len, M_sc, P_sc, R_sc,
+                                         M_minn, P_minn, R_minn, st);
+    if (frc != 0) return frc > 0 ? OFS_OK : frc;
+    const int rc = ofs_sc_metric(in_fmt, x, B, n_br, T, symbol_len, 1, precision, M_sc, P_sc, R_sc, stream);
+    if (rc) return rc;
+    return ofs_minn_metric(in_fmt, x, B, n_br, T, symbol_len, precision, M_minn, P_minn, R_minn, stream);
+}
+
+int32_t ofs_win_plan(int32_t kind, int32_t in_fmt, int32_t precision, int32_t n_br, int64_t T,
+                     int32_t symbol_len) {
+    if (kind == 4) return ofs_sc_minn_fast_plan(in_fmt, precision, n_br, T, symbol_len);
+    return ofs_win_fast_plan(kind, in_fmt, precision, n_br, T, symbol_len);
 }
 
 int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,

@@ -74,6 +74,25 @@ __device__ __forceinline__ int wave_min(int v) {
     return v;
 }
 
+// zero-filled DPP move (bound_ctrl): lanes without a source read 0
+template <int CTRL, int RMASK = 0xf>
+__device__ __forceinline__ double dppz(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RMASK, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RMASK, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+// inclusive wave64 prefix sum with zero-filled moves (no lane predicates)
+__device__ __forceinline__ double scan_add(double v) {
+    v += dppz<0x111>(v);            // row_shr:1
+    v += dppz<0x112>(v);            // row_shr:2
+    v += dppz<0x114>(v);            // row_shr:4
+    v += dppz<0x118>(v);            // row_shr:8
+    v += dppz<0x142, 0xa>(v);       // row_bcast:15 -> rows 1, 3
+    v += dppz<0x143, 0xc>(v);       // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ double shr1z(double v) { return dppz<0x138>(v); }   // wave_shr:1, lane 0 <- 0
+
 }  // namespace ofs
 
 // internal launchers implemented in aa_fast.hip (C++ linkage, not part of the ABI)
@@ -89,3 +108,17 @@ struct AaFastArgs {
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st);
 // 10*E + MR of the fast kernel a shape dispatches to, 0 if the general engine handles it
 int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L);
+
+// streaming fast path of the S&C / combined S&C / Minn window metrics (win_fast.hip)
+struct WinFastArgs {
+    const void* x; int64_t B, T; int N;
+    void* M; void* P; void* R;
+};
+// mode: 1 S&C (sc.py), 2 combined S&C (combined_sc_min.py), 3 Minn.  Returns 1 if launched,
+// 0 if the shape is not covered (caller uses the general engine), <0 on error.
+int ofs_win_fast_try(int mode, int fmt, int precision, int n_br, const WinFastArgs& a, hipStream_t st);
+int ofs_win_fast_plan(int mode, int fmt, int precision, int n_br, int64_t T, int N);
+// fused combined S&C + Minn (one pass): 10*E + MW, or 0
+int ofs_sc_minn_fast_plan(int fmt, int precision, int n_br, int64_t T, int N);
+int ofs_sc_minn_fast_try(int fmt, int precision, int n_br, const void* x, int64_t B, int64_t T, int N,
+                         void* Ms, void* Ps, void* Rs, void* Mm, void* Pm, void* Rm, hipStream_t st);

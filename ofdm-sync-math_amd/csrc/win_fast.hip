@@ -1,0 +1,455 @@
+// win_fast.hip — streaming fast path of the sliding-window timing metrics, fp32, any T:
+//   S&C            sc.sc_streaming_metric                       (sc.py:42-78)
+//   combined S&C   combined_sc_min.schmidl_cox_streaming_metric (combined_sc_min.py:116-164)
+//   Minn           minn.minn_streaming_metric(_parameterized)   (minn.py:59-112, :697-751)
+//
+// All three are window sums of one lagged product and of the energy, read at a few lags,
+// written in trailing form around the newest sample n = d + N - 1 (output index d):
+//   a(j) = x[j]·conj(x[j-D]),  S_a(n) = Σ_{j=n-W+1..n} a(j),  S_e(n) = Σ |x[j]|² (same window)
+//   S&C      (D = W = N/2):  P = conj(S_a(n)),  R = S_e(n)
+//   combined (D = W = N/2):  P = conj(S_a(n)),  R = S_e(n) + S_e(n-W)
+//   Minn     (D = W = N/4):  P = conj(S_a(n) + S_a(n-2W)),  R = S_e(n) + S_e(n-W) + S_e(n-2W)
+// (q0·conj(q1) = conj(a) over the window ending at d+2Q-1, etc.)
+//
+// Layout is the one of aa_fast.hip: one wave per stream, rows of RL = 64·E samples, lane l
+// owns samples RL·k + E·l + e, and with W = MW·RL every lag (D, W, 2W) lands in the SAME lane
+// and element MW or 2MW rows back — the lagged sample, the retained window suffix and the
+// window sums at n-W / n-2W live in register rings indexed by k mod (ring), resolved at
+// compile time by unrolling the row loop by the ring period.  Window sums use the
+// cancellation-free split S = suffix(row k-MW) + rows between (fp64 row totals) + prefix(row
+// k) of aa_fast.  Rows stream from HBM into registers one row ahead (software pipelined),
+// so the kernel handles streams of any length (cfg4: 4096 samples, N = 2048).
+#include "ofs_common.h"
+#include "ofdmsync.h"
+
+using namespace ofs;
+
+namespace {
+
+constexpr int WF_WG = 256;            // 4 waves = 4 streams per workgroup
+enum { WF_SC = 1, WF_COMB = 2, WF_MINN = 3 };
+
+template <int MODE, int E, int MW>
+__global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
+    constexpr int RL = 64 * E;
+    constexpr int W = MW * RL;
+    constexpr int N = (MODE == WF_MINN) ? 4 * W : 2 * W;
+    constexpr int HR = (MODE == WF_MINN) ? 2 * MW : MW;     // history ring rows (COMB / MINN)
+    constexpr int PD = 2;                                    // rows in flight ahead of use
+    constexpr int PER = HR > PD ? HR : PD;                   // unroll period (ring sizes divide it)
+    constexpr int V4 = E / 2;                                // float4 loads per lane per row
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * (WF_WG / 64) + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int64_t nout = T - N + 1;
+    const int nrows = (int)((T + RL - 1) / RL);
+    const float4* xs = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(a.x) + b * T);
+    float* Mo = reinterpret_cast<float*>(a.M) + b * nout;
+    float2* Po = reinterpret_cast<float2*>(a.P) + b * nout;
+    float* Ro = reinterpret_cast<float*>(a.R) + b * nout;
+
+    float lr[MW][E], li[MW][E];                  // x of rows k-MW..k-1 (lag D = W)
+    float sR[MW][E], sI[MW][E], sE[MW][E];       // retained in-window suffixes
+    float hR[HR][E], hI[HR][E], hE[HR][E];       // window sums of past rows (COMB/MINN)
+    double cbR[MW], cbI[MW], cbE[MW];            // row bases C[j] for j in (k-MW, k]
+    double CR = 0.0, CI = 0.0, CE = 0.0;         // C[k]: prefix at the start of row k
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+        cbR[m] = 0.0; cbI[m] = 0.0; cbE[m] = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { lr[m][e] = 0.f; li[m][e] = 0.f; sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f; }
+    }
+#pragma unroll
+    for (int m = 0; m < HR; ++m)
+#pragma unroll
+        for (int e = 0; e < E; ++e) { hR[m][e] = 0.f; hI[m][e] = 0.f; hE[m][e] = 0.f; }
+
+    float4 nx[PD][V4];
+    auto load_row = [&](int k, float4 (&dst)[V4]) {
+#pragma unroll
+        for (int j = 0; j < V4; ++j) {
+            int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;       // float4 index (2 samples)
+            const int64_t qmax = T / 2 - 1;
+            dst[j] = xs[q < qmax ? q : qmax];                       // zeroed on use past T
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load_row(p < nrows ? p : 0, nx[p]);
+
+    for (int k0 = 0; k0 < nrows; k0 += PER) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = k0 + u;
+            if (k < nrows) {
+                const int64_t nb = (int64_t)RL * k + E * lane;
+                float cr[E], ci[E];
+#pragma unroll
+                for (int j = 0; j < V4; ++j) {
+                    const bool ok = nb + 2 * j < T;                 // T even: pairs are whole
+                    const float4 v = nx[u % PD][j];
+                    cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
+                    cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
+                }
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);   // PD rows ahead
+                // ---- lagged products and energies (fp32) ----
+                const int sl = u % MW;                              // ring slot of row k (and k-MW)
+                float aR[E], aI[E], aE[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    aE[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                    if (k >= MW) {
+                        aR[e] = fmaf(cr[e], lr[sl][e], ci[e] * li[sl][e]);
+                        aI[e] = fmaf(ci[e], lr[sl][e], -(cr[e] * li[sl][e]));
+                    } else {
+                        aR[e] = 0.f; aI[e] = 0.f;
+                    }
+                    lr[sl][e] = cr[e]; li[sl][e] = ci[e];
+                }
+                // ---- in-lane partials (forward f, backward g) ----
+                float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
+                fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+#pragma unroll
+                for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
+                gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+#pragma unroll
+                for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+                // ---- lane totals: fp64 wave scan; row totals; rows strictly inside the window ----
+                const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
+                const double tR = readlane(iR, 63), tI = readlane(iI, 63), tE = readlane(iE, 63);
+                const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);
+                const float uR = (float)(tR - iR), uI = (float)(tI - iI), uE = (float)(tE - iE);
+                const int so = (u + 1) % MW;                        // slot of C[k-MW+1]
+                const float wR = (float)(k >= MW ? CR - cbR[so] : CR);
+                const float wI = (float)(k >= MW ? CI - cbI[so] : CI);
+                const float wE = (float)(k >= MW ? CE - cbE[so] : CE);
+                // ---- window sums, outputs ----
+                float oM[E], oPr[E], oPi[E], oR[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float SR = wR + (xR + fR[e]), SI = wI + (xI + fI[e]), SE = wE + (xE + fE[e]);
+                    if (k >= MW) { SR += sR[sl][e]; SI += sI[sl][e]; SE += sE[sl][e]; }
+                    sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
+                    float PR = SR, PI = SI, RR = SE;
+                    if constexpr (MODE == WF_COMB) {
+                        RR += hE[sl][e];                            // S_e(n - W): row k-MW
+                        hE[sl][e] = SE;
+                    } else if constexpr (MODE == WF_MINN) {
+                        const int h2 = u % HR;                      // row k-2MW (and k)
+                        const int h1 = (u + MW) % HR;               // row k-MW
+                        PR += hR[h2][e]; PI += hI[h2][e];
+                        RR += hE[h1][e] + hE[h2][e];
+                        hR[h2][e] = SR; hI[h2][e] = SI; hE[h2][e] = SE;
+                    }
+                    PI = -PI;                                       // P = conj(window sum)
+                    const float den = fmaxf(RR, 1e-12f);
+                    const float num = (MODE == WF_MINN) ? fmaxf(PR, 0.f) * fmaxf(PR, 0.f) : fmaf(PR, PR, PI * PI);
+                    oM[e] = num / (den * den);
+                    oPr[e] = PR; oPi[e] = PI; oR[e] = RR;
+                }
+                // C[k+1] replaces C[k-MW+1] in the ring
+                cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
+                CR += tR; CI += tI; CE += tE;
+                // ---- stores: outputs d = n - (N-1) in [0, nout) ----
+                // a lane's E outputs are contiguous: dword-aligned vector stores (the output
+                // rows [B][T-N+1] are not 16-byte aligned; gfx950 global stores allow it)
+                const int64_t d0 = nb - (N - 1);
+                if (d0 >= 0 && d0 + E <= nout) {
+#pragma unroll
+                    for (int j = 0; j < E; j += 4) {
+                        if constexpr (E >= 4) {
+                            if (a.M) *reinterpret_cast<float4*>(Mo + d0 + j) = make_float4(oM[j], oM[j + 1], oM[j + 2], oM[j + 3]);
+                            if (a.R) *reinterpret_cast<float4*>(Ro + d0 + j) = make_float4(oR[j], oR[j + 1], oR[j + 2], oR[j + 3]);
+                        }
+                    }
+                    if constexpr (E < 4) {
+#pragma unroll
+                        for (int j = 0; j < E; j += 2) {
+                            if (a.M) *reinterpret_cast<float2*>(Mo + d0 + j) = make_float2(oM[j], oM[j + 1]);
+                            if (a.R) *reinterpret_cast<float2*>(Ro + d0 + j) = make_float2(oR[j], oR[j + 1]);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < E; j += 2)
+                        if (a.P) *reinterpret_cast<float4*>(Po + d0 + j) = make_float4(oPr[j], oPi[j], oPr[j + 1], oPi[j + 1]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int64_t d = d0 + e;
+                        if (d >= 0 && d < nout) {
+                            if (a.M) Mo[d] = oM[e];
+                            if (a.P) Po[d] = make_float2(oPr[e], oPi[e]);
+                            if (a.R) Ro[d] = oR[e];
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused combined_sc_min detector (cfg4): combined S&C (D = W = 2Q, R over both halves) AND
+// Minn (D = W = Q) from ONE pass over the stream, N = 4Q.  Lags in rows: Q = MW rows.
+//   S&C : P = conj(S_h(n)),            R = S_e(n) + S_e(n-Q) + S_e(n-2Q) + S_e(n-3Q)
+//   Minn: P = conj(S_q(n) + S_q(n-2Q)), R = S_e(n) + S_e(n-Q) + S_e(n-2Q)
+// with S_h / S_q the lag-2Q / lag-Q product windows and S_e the Q-window energy.  The x ring
+// (2MW rows) and the window suffixes stay in registers; the per-row histories of S_e and S_q
+// (read back Q..3Q later) live in a per-wave LDS slice (no barriers: one wave owns it).
+// ------------------------------------------------------------------------------------------
+struct WinFusedArgs {
+    const void* x; int64_t B, T; int N;
+    float* Ms; float2* Ps; float* Rs; float* Mm; float2* Pm; float* Rm;
+};
+
+template <int E, int MW>
+__global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
+    constexpr int RL = 64 * E;
+    constexpr int N = 4 * MW * RL;
+    constexpr int XR = 2 * MW;                  // x ring / S_h suffix ring / S_q history ring
+    constexpr int ER = 4 * MW;                  // S_e history ring
+    constexpr int PD = 2;
+    constexpr int PER = ER;
+    constexpr int V4 = E / 2;
+    __shared__ float hist[WF_WG / 64][ER + 2 * XR][E][64];   // [S_e rows | S_q re rows | S_q im rows]
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * (WF_WG / 64) + w;
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int64_t nout = T - N + 1;
+    const int nrows = (int)((T + RL - 1) / RL);
+    const float4* xs = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(a.x) + b * T);
+
+    float xr_[XR][E], xi_[XR][E];
+    float shR[XR][E], shI[XR][E];               // S_h suffixes (window 2Q = XR rows)
+    float sqR[MW][E], sqI[MW][E], seE[MW][E];   // S_q, S_e suffixes (window Q = MW rows)
+    double chR[XR], chI[XR], cqR[MW], cqI[MW], ceE[MW];
+    double CHR = 0, CHI = 0, CQR = 0, CQI = 0, CEE = 0;
+#pragma unroll
+    for (int m = 0; m < XR; ++m) {
+        chR[m] = 0; chI[m] = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { xr_[m][e] = 0.f; xi_[m][e] = 0.f; shR[m][e] = 0.f; shI[m][e] = 0.f; }
+    }
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+        cqR[m] = 0; cqI[m] = 0; ceE[m] = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sqR[m][e] = 0.f; sqI[m][e] = 0.f; seE[m][e] = 0.f; }
+    }
+    auto H = [&](int row, int e) -> float& { return hist[w][row][e][lane]; };
+
+    float4 nx[PD][V4];
+    auto load_row = [&](int k, float4 (&dst)[V4]) {
+#pragma unroll
+        for (int j = 0; j < V4; ++j) {
+            const int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;
+            const int64_t qmax = T / 2 - 1;
+            dst[j] = xs[q < qmax ? q : qmax];
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load_row(p < nrows ? p : 0, nx[p]);
+
+    // in-lane forward/backward partials + fp64 wave scan of one quantity
+    struct Part { float f[E], g[E]; float xe, us; double tot; };
+    auto part = [&](const float (&v)[E], Part& p) {
+        p.f[0] = v[0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) p.f[e] = p.f[e - 1] + v[e];
+        p.g[E - 1] = 0.f;
+#pragma unroll
+        for (int e = E - 2; e >= 0; --e) p.g[e] = p.g[e + 1] + v[e + 1];
+        const double i = scan_add((double)p.f[E - 1]);
+        p.tot = readlane(i, 63);
+        p.xe = (float)shr1z(i);
+        p.us = (float)(p.tot - i);
+    };
+
+    for (int k0 = 0; k0 < nrows; k0 += PER) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = k0 + u;
+            if (k < nrows) {
+                const int64_t nb = (int64_t)RL * k + E * lane;
+                float cr[E], ci[E];
+#pragma unroll
+                for (int j = 0; j < V4; ++j) {
+                    const bool ok = nb + 2 * j < T;
+                    const float4 v = nx[u % PD][j];
+                    cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
+                    cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
+                }
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
+                const int x2 = u % XR;                 // row k-2MW (x ring), then row k
+                const int x1 = (u + MW) % XR;          // row k-MW
+                float hR[E], hI[E], qR[E], qI[E], en[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    en[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                    const float d2r = xr_[x2][e], d2i = xi_[x2][e], d1r = xr_[x1][e], d1i = xi_[x1][e];
+                    hR[e] = fmaf(cr[e], d2r, ci[e] * d2i); hI[e] = fmaf(ci[e], d2r, -(cr[e] * d2i));
+                    qR[e] = fmaf(cr[e], d1r, ci[e] * d1i); qI[e] = fmaf(ci[e], d1r, -(cr[e] * d1i));
+                    xr_[x2][e] = cr[e]; xi_[x2][e] = ci[e];
+                }
+                Part ph_r, ph_i, pq_r, pq_i, pe;
+                part(hR, ph_r); part(hI, ph_i); part(qR, pq_r); part(qI, pq_i); part(en, pe);
+                const int sq = u % MW, soq = (u + 1) % MW, soh = (u + 1) % XR;
+                const float whR = (float)(k >= XR ? CHR - chR[soh] : CHR);
+                const float whI = (float)(k >= XR ? CHI - chI[soh] : CHI);
+                const float wqR = (float)(k >= MW ? CQR - cqR[soq] : CQR);
+                const float wqI = (float)(k >= MW ? CQI - cqI[soq] : CQI);
+                const float weE = (float)(k >= MW ? CEE - ceE[soq] : CEE);
+                const int e0 = u % ER, e1 = (u + 3 * MW) % ER, e2 = (u + 2 * MW) % ER, e3 = (u + MW) % ER;
+                float oMs[E], oRs[E], oMm[E], oRm[E], oPsr[E], oPsi[E], oPmr[E], oPmi[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float SHR = whR + (ph_r.xe + ph_r.f[e]), SHI = whI + (ph_i.xe + ph_i.f[e]);
+                    float SQR = wqR + (pq_r.xe + pq_r.f[e]), SQI = wqI + (pq_i.xe + pq_i.f[e]);
+                    float SE = weE + (pe.xe + pe.f[e]);
+                    if (k >= XR) { SHR += shR[x2][e]; SHI += shI[x2][e]; }
+                    if (k >= MW) { SQR += sqR[sq][e]; SQI += sqI[sq][e]; SE += seE[sq][e]; }
+                    shR[x2][e] = ph_r.us + ph_r.g[e]; shI[x2][e] = ph_i.us + ph_i.g[e];
+                    sqR[sq][e] = pq_r.us + pq_r.g[e]; sqI[sq][e] = pq_i.us + pq_i.g[e];
+                    seE[sq][e] = pe.us + pe.g[e];
+                    // histories (LDS): S_e rows k-MW, k-2MW, k-3MW; S_q row k-2MW
+                    const float E1 = H(e1, e), E2 = H(e2, e), E3 = H(e3, e);
+                    const float Q2r = H(ER + x2, e), Q2i = H(ER + XR + x2, e);
+                    H(e0, e) = SE; H(ER + x2, e) = SQR; H(ER + XR + x2, e) = SQI;
+                    const float Rm = SE + E1 + E2;
+                    const float Rs = Rm + E3;
+                    const float Pmr = SQR + Q2r, Pmi = -(SQI + Q2i);
+                    const float Psr = SHR, Psi = -SHI;
+                    const float ds = fmaxf(Rs, 1e-12f), dm = fmaxf(Rm, 1e-12f);
+                    oMs[e] = fmaf(Psr, Psr, Psi * Psi) / (ds * ds);
+                    oMm[e] = (fmaxf(Pmr, 0.f) * fmaxf(Pmr, 0.f)) / (dm * dm);
+                    oRs[e] = Rs; oRm[e] = Rm; oPsr[e] = Psr; oPsi[e] = Psi; oPmr[e] = Pmr; oPmi[e] = Pmi;
+                }
+                chR[soh] = CHR + ph_r.tot; chI[soh] = CHI + ph_i.tot;
+                cqR[soq] = CQR + pq_r.tot; cqI[soq] = CQI + pq_i.tot; ceE[soq] = CEE + pe.tot;
+                CHR += ph_r.tot; CHI += ph_i.tot; CQR += pq_r.tot; CQI += pq_i.tot; CEE += pe.tot;
+                const int64_t d0 = nb - (N - 1);
+                auto put = [&](float* Mo, float2* Po, float* Ro, const float (&m)[E], const float (&pr)[E],
+                               const float (&pi)[E], const float (&r)[E]) {
+                    Mo += b * nout; Po += b * nout; Ro += b * nout;
+                    if (d0 >= 0 && d0 + E <= nout) {
+#pragma unroll
+                        for (int j = 0; j < E; j += 2) {
+                            if (Mo) *reinterpret_cast<float2*>(Mo + d0 + j) = make_float2(m[j], m[j + 1]);
+                            if (Ro) *reinterpret_cast<float2*>(Ro + d0 + j) = make_float2(r[j], r[j + 1]);
+                            if (Po) *reinterpret_cast<float4*>(Po + d0 + j) = make_float4(pr[j], pi[j], pr[j + 1], pi[j + 1]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int64_t d = d0 + e;
+                            if (d >= 0 && d < nout) {
+                                if (Mo) Mo[d] = m[e];
+                                if (Po) Po[d] = make_float2(pr[e], pi[e]);
+                                if (Ro) Ro[d] = r[e];
+                            }
+                        }
+                    }
+                };
+                put(a.Ms, a.Ps, a.Rs, oMs, oPsr, oPsi, oRs);
+                put(a.Mm, a.Pm, a.Rm, oMm, oPmr, oPmi, oRm);
+            }
+        }
+    }
+}
+
+template <int MODE, int E, int MW>
+int launch(const WinFastArgs& a, hipStream_t st) {
+    const int64_t grid = (a.B + 3) / 4;
+    hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
+
+template <int MODE, int E>
+int launch_mw(int mw, const WinFastArgs& a, hipStream_t st) {
+    switch (mw) {
+        case 1: return launch<MODE, E, 1>(a, st);
+        case 2: return launch<MODE, E, 2>(a, st);
+        case 4: return launch<MODE, E, 4>(a, st);
+        case 8: return launch<MODE, E, 8>(a, st);
+    }
+    return 0;
+}
+
+template <int MODE>
+int launch_e(int e, int mw, const WinFastArgs& a, hipStream_t st) {
+    switch (e) {
+        case 2: return launch_mw<MODE, 2>(mw, a, st);
+        case 4: return launch_mw<MODE, 4>(mw, a, st);
+    }
+    return 0;
+}
+
+// samples per lane per row E and window rows MW for window W, or E = 0 if not covered
+void pick(int W, int& E, int& mw) {
+    // prefer short register rings (MW <= 4), then wider rows
+    E = 0; mw = 0;
+    for (int pass = 0; pass < 2; ++pass)
+        for (int e : {4, 2}) {
+            const int rl = 64 * e;
+            if (W % rl) continue;
+            const int m = W / rl;
+            if ((pass == 0 && (m == 1 || m == 2 || m == 4)) || (pass == 1 && m == 8)) { E = e; mw = m; return; }
+        }
+}
+
+template <int E, int MW>
+int launch_fused(const WinFusedArgs& a, hipStream_t st) {
+    const int64_t grid = (a.B + 3) / 4;
+    hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
+
+}  // namespace
+
+int ofs_sc_minn_fast_plan(int fmt, int precision, int n_br, int64_t T, int N) {
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br != 1 || (T & 1) || T < N || N % 4) return 0;
+    const int Q = N / 4;
+    for (int e : {4, 2}) {                     // per-wave LDS history: 64·E·(8·MW) floats
+        if (Q % (64 * e)) continue;
+        const int m = Q / (64 * e);
+        if (m == 1 || m == 2 || (m == 4 && e == 2)) return 10 * e + m;
+    }
+    return 0;
+}
+
+int ofs_sc_minn_fast_try(int fmt, int precision, int n_br, const void* x, int64_t B, int64_t T, int N,
+                         void* Ms, void* Ps, void* Rs, void* Mm, void* Pm, void* Rm, hipStream_t st) {
+    const int plan = ofs_sc_minn_fast_plan(fmt, precision, n_br, T, N);
+    if (!plan) return 0;
+    const WinFusedArgs a{x, B, T, N, (float*)Ms, (float2*)Ps, (float*)Rs, (float*)Mm, (float2*)Pm, (float*)Rm};
+    switch (plan) {
+        case 41: return launch_fused<4, 1>(a, st);
+        case 42: return launch_fused<4, 2>(a, st);
+        case 21: return launch_fused<2, 1>(a, st);
+        case 22: return launch_fused<2, 2>(a, st);
+        default: return launch_fused<2, 4>(a, st);
+    }
+}
+
+int ofs_win_fast_plan(int mode, int fmt, int precision, int n_br, int64_t T, int N) {
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br != 1 || (T & 1) || T < N) return 0;
+    if (mode < WF_SC || mode > WF_MINN) return 0;
+    const int div = mode == WF_MINN ? 4 : 2;
+    if (N % div) return 0;
+    int E, mw;
+    pick(N / div, E, mw);
+    return E ? 10 * E + mw : 0;
+}
+
+int ofs_win_fast_try(int mode, int fmt, int precision, int n_br, const WinFastArgs& a, hipStream_t st) {
+    const int plan = ofs_win_fast_plan(mode, fmt, precision, n_br, a.T, a.N);
+    if (!plan) return 0;
+    const int E = plan / 10, mw = plan % 10;
+    switch (mode) {
+        case WF_SC: return launch_e<WF_SC>(E, mw, a, st);
+        case WF_COMB: return launch_e<WF_COMB>(E, mw, a, st);
+        default: return launch_e<WF_MINN>(E, mw, a, st);
+    }
+}

@@ -47,7 +47,11 @@ def _declare(lib):
         "ofs_zc_correlate": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_double,
                                        c_int32, P, P, P, P]),
         "ofs_zc_freq_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
-                                         c_int32, P, P, c_double, P, P]),
+                                         c_int32, c_int32, P, P, c_double, P, P]),
+        "ofs_sc_minn_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P,
+                                         P, P, P, P, P]),
+        "ofs_win_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int64, c_int32]),
+        "ofs_zc_freq_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32, c_int32]),
         "ofs_zc_detect": (c_int32, [P, c_int64, c_int64, c_int32, c_int64, c_int32, c_double, c_int32,
                                     c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),
         "ofs_zc_gate": (c_int32, [P, P, P, c_int64, c_int64, c_int32, c_int32, P, c_int32, P, P, P,

@@ -29,3 +29,28 @@ def schmidl_cox_streaming_metric_batched(x, symbol_len: int = N_FFT, *, precisio
 def minn_streaming_metric_batched(x, symbol_len: int | None = None, *, precision=None):
     return window_metric("minn", x, N_FFT if symbol_len is None else symbol_len, batched=True,
                          precision=precision)
+
+
+def sc_minn_streaming_metrics_batched(x, symbol_len: int | None = None, *, precision=None):
+    """Both detector metrics of combined_sc_min.run_simulation (combined_sc_min.py:333-334) in
+    one pass: ((M_minn, P_minn, R_minn), (M_sc, P_sc, R_sc)), device tensors [B, T-N+1].
+    Runs the fused kernel (``ofs_sc_minn_metric``) where it applies."""
+    import torch
+
+    from . import _lib
+    N = int(N_FFT if symbol_len is None else symbol_len)
+    batch = _lib.as_batch(x, batched=True)
+    prec = _lib.resolve_precision(batch, precision)
+    dev = batch.data.device
+    if N % 2:
+        raise ValueError(f"operands could not be broadcast together: odd symbol length {N}")
+    n_out = max(batch.T - N + 1, 0)
+    outs = [_lib.out_real((batch.B, n_out), prec, dev), _lib.out_cplx((batch.B, n_out), prec, dev),
+            _lib.out_real((batch.B, n_out), prec, dev), _lib.out_real((batch.B, n_out), prec, dev),
+            _lib.out_cplx((batch.B, n_out), prec, dev), _lib.out_real((batch.B, n_out), prec, dev)]
+    if n_out > 0 and batch.B > 0:
+        rc = _lib.lib().ofs_sc_minn_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, N,
+                                           prec, *[t.data_ptr() for t in outs], _lib.stream_ptr())
+        _lib.check(rc, "ofs_sc_minn_metric")
+    del torch
+    return (outs[3], outs[4], outs[5]), (outs[0], outs[1], outs[2])

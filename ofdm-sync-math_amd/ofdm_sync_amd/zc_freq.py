@@ -38,7 +38,8 @@ def make_pss_frequency_template() -> tuple[np.ndarray, np.ndarray, float]:
     return bin_indices, template_bins, energy
 
 
-def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, template_energy):
+def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, template_energy,
+         precision=None):
     idx = np.ascontiguousarray(np.asarray(bin_indices).astype(np.int32))
     tb = np.ascontiguousarray(np.asarray(template_bins, dtype=np.complex128))
     if idx.ndim != 1 or tb.shape != idx.shape:
@@ -48,28 +49,39 @@ def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, templat
     noff = batch.T - (N + cp) + 1
     if noff <= 0:
         raise ValueError("Received stream is shorter than a single OFDM symbol.")
-    if batch.nb > 4:
-        raise ValueError("ofs_zc_freq_metric supports up to 4 receive branches")
-    out = torch.empty((batch.B, noff), dtype=torch.float64, device=batch.data.device)
-    rc = _lib.lib().ofs_zc_freq_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T,
-                                       int(N), int(cp), int(idx.size), idx.ctypes.data, tb.ctypes.data,
-                                       float(template_energy), out.data_ptr(), _lib.stream_ptr())
+    L = _lib.lib()
+    prec = _lib.resolve_precision(batch, precision)
+    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) != 2:
+        if precision is not None:
+            raise ValueError("fp32 zc_freq needs complex64 input, N = 64*2^j <= 4096 and <= 64 "
+                             "offsets per stream (the window-FFT kernel); use precision='fp64'")
+        prec = _lib.FP64                          # auto: the fp64 sliding-DFT kernel
+    if prec == _lib.FP64 and batch.nb > 4:
+        raise ValueError("the fp64 zc_freq kernel supports up to 4 receive branches")
+    out = torch.empty((batch.B, noff), dtype=torch.float64 if prec == _lib.FP64 else torch.float32,
+                      device=batch.data.device)
+    rc = L.ofs_zc_freq_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, int(N),
+                              int(cp), prec, int(idx.size), idx.ctypes.data, tb.ctypes.data,
+                              float(template_energy), out.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "ofs_zc_freq_metric")
     return out
 
 
-def compute_frequency_metric(rx_samples, bin_indices, template_bins, template_energy: float):
+def compute_frequency_metric(rx_samples, bin_indices, template_bins, template_energy: float, *,
+                             precision=None):
     """Evaluate the LTE-style frequency-domain metric across all offsets (zc_freq.py:62-99)."""
     batch = _lib.as_batch(rx_samples, batched=False)
-    out = _run(batch, int(N_FFT), int(CYCLIC_PREFIX), bin_indices, template_bins, template_energy)
+    out = _run(batch, int(N_FFT), int(CYCLIC_PREFIX), bin_indices, template_bins, template_energy,
+               precision)
     return _lib.to_host(out[0], np.float64) if batch.from_numpy else out[0]
 
 
 def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, template_energy=None,
-                                     N: int | None = None, cp: int | None = None):
-    """Batched metric over x[B, n_branch, T] -> device tensor [B, T-(N+cp)+1] (f64)."""
+                                     N: int | None = None, cp: int | None = None, *, precision=None):
+    """Batched metric over x[B, n_branch, T] -> device tensor [B, T-(N+cp)+1]: f64 (sliding
+    DFT) or, for complex64 input with few offsets per stream, f32 (window FFT)."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
     return _run(batch, int(N_FFT if N is None else N), int(CYCLIC_PREFIX if cp is None else cp),
-                bin_indices, template_bins, template_energy)
+                bin_indices, template_bins, template_energy, precision)

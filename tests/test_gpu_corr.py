@@ -246,3 +246,36 @@ def test_zc_combined_batched_vs_oracle():
         co = O.zc_combined(x[b], ref)
         assert rel(corr[b].cpu().numpy(), co) < 1e-11
         np.testing.assert_allclose(mag[b].cpu().numpy(), np.abs(co), rtol=1e-11, atol=1e-14)
+
+
+@pytest.mark.parametrize("N,cp,T,nb", [(4096, 0, 4096, 1), (4096, 512, 4620, 2), (2048, 0, 2048, 1),
+                                       (1024, 256, 1300, 1), (256, 64, 330, 3), (128, 0, 190, 1)])
+def test_zc_freq_fp32_window_fft_vs_oracle(N, cp, T, nb):
+    """cfg5 shape (few windows per sequence, complex64): the fp32 window-FFT kernel.
+    Tolerance: metric (a ratio in [0, 1]) within 2e-5 absolute."""
+    from ofdm_sync_amd import _lib
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 2
+    rng = np.random.default_rng(N + nb)
+    B = 40
+    x = rng_c(rng, B, nb, T)
+    sym = O.pss_symbol(N)
+    for b in range(0, B, 3):                       # every third stream carries the PSS symbol
+        x[b, :, cp + (b % 5):cp + (b % 5) + N] += rng.uniform(0.5, 8.0) * sym[:min(N, T - cp - b % 5)]
+    x = x.astype(np.complex64)
+    idx, t, e = O.zc_template()
+    m = zc_freq.compute_frequency_metric_batched(torch.from_numpy(x).cuda(), idx, t, e, N=N, cp=cp)
+    assert m.dtype == torch.float32
+    mm = m.cpu().numpy()
+    for b in range(B):
+        mo = O.zc_freq_metric(x[b].astype(np.complex128), N, cp, idx, t, e)
+        np.testing.assert_allclose(mm[b], mo, rtol=0, atol=2e-5)
+    assert mm.max() > 0.5                          # the PSS windows light up
+
+
+def test_zc_freq_fp32_unsupported_shape_raises():
+    x = torch.zeros((1, 1, 5000), dtype=torch.complex64, device="cuda")
+    idx, t, e = O.zc_template()
+    with pytest.raises(ValueError):                # > 64 offsets per stream: no fp32 kernel
+        zc_freq.compute_frequency_metric_batched(x, idx, t, e, N=2048, cp=0, precision="fp32")
+    m = zc_freq.compute_frequency_metric_batched(x, idx, t, e, N=2048, cp=0)   # auto -> fp64
+    assert m.dtype == torch.float64

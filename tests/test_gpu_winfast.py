@@ -1,0 +1,98 @@
+"""GPU parity of the streaming fp32 fast path for the S&C / combined S&C / Minn window
+metrics (csrc/win_fast.hip) against the CPU oracle (fp64), through the C ABI.
+
+Tolerance (fp32 path, complex64 input, north_star): M within 1e-6 (absolute for M <= 1,
+relative above: the S&C-with-second-half-R and Minn metrics are not bounded by 1 — a quiet
+window after a loud one reaches M ~ 200); P and R within 1e-5 of the stream maximum.  The
+dispatch is asserted to be the fast kernel.
+"""
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from ofdm_sync_amd import _lib, sc, combined_sc_min, minn, synth  # noqa: E402
+
+KIND = {"sc": 1, "comb": 2, "minn": 3}
+ORACLE = {"sc": O.sc_metric, "comb": O.comb_sc_metric, "minn": O.minn_metric}
+
+
+def run(kind, x, N):
+    if kind == "sc":
+        return sc.sc_streaming_metric_batched(x, N)
+    if kind == "comb":
+        return combined_sc_min.schmidl_cox_streaming_metric_batched(x, N)
+    return minn.minn_streaming_metric_batched(x, N)
+
+
+def m_ok(m, mo):
+    return bool(np.all(np.abs(m - mo) <= 1e-6 * np.maximum(1.0, np.abs(mo))))
+
+
+def relerr(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+@pytest.mark.parametrize("kind", ["sc", "comb", "minn"])
+@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 1024), (1024, 3000), (512, 700), (256, 1024),
+                                 (4096, 6000), (2048, 2048)])
+def test_window_fast_path_vs_oracle(kind, N, T):
+    plan = _lib.lib().ofs_win_plan(KIND[kind], _lib.C64, _lib.FP32, 1, T, N)
+    # Minn N=256 (Q=64) is below the fast kernel's 128-sample row: general engine
+    assert (plan == 0) if (kind == "minn" and N == 256) else (plan > 0), plan
+    B = 6
+    x = synth.make_aa_batch(B, T, min(N // 2 if kind != "minn" else N // 4, 1024), seed=N + T, device="cuda")
+    x[3, :, : T // 3] *= 1e-3                      # quiet span before a loud one
+    x[4, :, T // 2:] *= 1e-3                       # and after one
+    M, P, R = run(kind, x, N)
+    assert M.dtype == torch.float32 and M.shape == (B, T - N + 1)
+    xh = x.cpu().numpy().astype(np.complex128)
+    for b in range(B):
+        Mo, Po, Ro = ORACLE[kind](xh[b], N)
+        assert m_ok(M[b].cpu().numpy(), Mo)
+        assert relerr(P[b].cpu().numpy(), Po) < 1e-5
+        assert relerr(R[b].cpu().numpy(), Ro) < 1e-5
+
+
+def test_window_fast_path_covers_cfg4():
+    L = _lib.lib()
+    assert L.ofs_win_plan(2, _lib.C64, _lib.FP32, 1, 4096, 2048) > 0
+    assert L.ofs_win_plan(3, _lib.C64, _lib.FP32, 1, 4096, 2048) > 0
+    assert L.ofs_win_plan(1, _lib.C64, _lib.FP32, 2, 4096, 2048) == 0      # 2 branches: general
+    assert L.ofs_win_plan(1, _lib.C128, _lib.FP64, 1, 4096, 2048) == 0     # fp64: general
+
+
+@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 1024), (512, 1500), (256, 800), (2048, 2100)])
+def test_fused_sc_minn_vs_oracle(N, T):
+    """combined_sc_min's two metrics from the fused one-pass kernel (cfg4 shape first)."""
+    plan = _lib.lib().ofs_win_plan(4, _lib.C64, _lib.FP32, 1, T, N)
+    assert (plan == 0) if N == 256 else (plan > 0), plan     # Q=64 < one 128-sample row
+    B = 6
+    x = synth.make_aa_batch(B, T, min(N // 2, 1024), seed=N + 3 * T, device="cuda")
+    x[2, :, T // 2:] *= 1e-3
+    (Mm, Pm, Rm), (Ms, Ps, Rs) = combined_sc_min.sc_minn_streaming_metrics_batched(x, N)
+    xh = x.cpu().numpy().astype(np.complex128)
+    for b in range(B):
+        Mo, Po, Ro = O.minn_metric(xh[b], N)
+        assert m_ok(Mm[b].cpu().numpy(), Mo)
+        assert relerr(Pm[b].cpu().numpy(), Po) < 1e-5 and relerr(Rm[b].cpu().numpy(), Ro) < 1e-5
+        Mo, Po, Ro = O.comb_sc_metric(xh[b], N)
+        assert m_ok(Ms[b].cpu().numpy(), Mo)
+        assert relerr(Ps[b].cpu().numpy(), Po) < 1e-5 and relerr(Rs[b].cpu().numpy(), Ro) < 1e-5
+
+
+def test_fused_sc_minn_general_fallback_fp64():
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((2, 2, 900)) + 1j * rng.standard_normal((2, 2, 900))
+    (Mm, Pm, Rm), (Ms, Ps, Rs) = combined_sc_min.sc_minn_streaming_metrics_batched(torch.from_numpy(x).cuda(), 256)
+    for b in range(2):
+        Mo, _, _ = O.minn_metric(x[b], 256)
+        np.testing.assert_allclose(Mm[b].cpu().numpy(), Mo, rtol=1e-9, atol=1e-12)
+        Mo, _, _ = O.comb_sc_metric(x[b], 256)
+        np.testing.assert_allclose(Ms[b].cpu().numpy(), Mo, rtol=1e-9, atol=1e-12)

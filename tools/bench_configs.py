@@ -1,0 +1,171 @@
+"""Secondary BASELINE.json configurations (cfg2, cfg4, cfg5) on one GPU.
+
+bench.py measures the headline (cfg3).  This script times the other configs named in
+BASELINE.json with the same method (warm-up, then K launches bracketed by HIP events on the
+launch stream, inputs resident in HBM) and prints one JSON line per config with the
+algorithmic bytes per launch and the achieved fraction of the
+8 TB/s HBM peak.  Synthetic inputs of the config's shape; not the driver's headline line.
+
+    python tools/bench_configs.py [--configs cfg2a,cfg2b,cfg4,cfg5] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ofdm_sync_amd import _lib, synth, zc_freq  # noqa: E402
+
+HBM = 8000.0
+
+
+def timed(step, steps, warmup, stream):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def chk(rc, what):
+    if rc:
+        raise RuntimeError(f"{what}: status {rc}")
+
+
+def int12(x):
+    s = 2046.0 / float(x.abs().amax())
+    re = torch.clamp(torch.round(x.real * s), -2048, 2047).to(torch.int16)
+    im = torch.clamp(torch.round(x.imag * s), -2048, 2047).to(torch.int16)
+    return torch.stack([re, im], dim=-1).contiguous()
+
+
+def cfg2a(dev, st, steps, warmup):
+    """cfg2 (aa side): sync_aa detector, L=128, int12 I/Q, B=4096 x T=1024, fp64 (bit-exact)."""
+    B, T, L = 4096, 1024, 128
+    x = int12(synth.make_aa_batch(B, T, L, seed=7, device=dev))
+    P = torch.empty((B, T), dtype=torch.complex128, device=dev)
+    R = torch.empty((B, T), dtype=torch.float64, device=dev)
+    M = torch.empty_like(R)
+    V = torch.empty((B, T), dtype=torch.uint8, device=dev)
+    E = 4
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.CI16, x.data_ptr(), B, 1, T, L, _lib.FP64, P.data_ptr(), R.data_ptr(), M.data_ptr(),
+            V.data_ptr(), 1, 0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(),
+            st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa"), steps, warmup, st)
+    nbytes = B * T * (4 + 16 + 8 + 8 + 1)
+    return dict(config="cfg2a", workload=f"sync_aa detector L={L}, int12 I/Q, {B} x {T}, fp64",
+                kernel="win_kernel<CI16,fp64,AA> (fused events)", samples=B * T, ms=ms, alg_bytes=nbytes,
+                bytes_per_sample="4 in + P 16 + R 8 + M 8 + valid 1")
+
+
+def cfg2b(dev, st, steps, warmup):
+    """cfg2 (minn_rtl side): Q=64, int12 I/Q, B=4096 x T=1024, fused IIR + threshold + gate."""
+    B, T, Q = 4096, 1024, 64
+    x = int12(synth.make_aa_batch(B, T, 128, seed=9, device=dev))
+    f = lambda: torch.empty((B, T), dtype=torch.float64, device=dev)   # noqa: E731
+    b = lambda: torch.empty((B, T), dtype=torch.bool, device=dev)      # noqa: E731
+    o = [f(), f(), f(), f(), f(), f(), b(), b()]
+    E = 16
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    og = torch.empty(B, dtype=torch.int64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.CI16, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *[t.data_ptr() for t in o], 1, 2, 0, E,
+            n_ev.data_ptr(), ev.data_ptr(), og.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_minn_rtl(*args), "minn_rtl"), steps, warmup, st)
+    nbytes = B * T * (4 + 6 * 8 + 2)
+    return dict(config="cfg2b", workload=f"minn_rtl Q={Q}, int12 I/Q, {B} x {T}, fp64 + sequential IIR/gate",
+                kernel="win_kernel<CI16,fp64,RTL> + rtl_iir_kernel", samples=B * T, ms=ms, alg_bytes=nbytes,
+                bytes_per_sample="4 in + 6 x f64 8 + 2 flags")
+
+
+def cfg4(dev, st, steps, warmup):
+    """cfg4 per-GPU shard: combined S&C (both-halves R) + Minn, N=2048, 32768 x 4096 c64, fp32."""
+    B, T, N = 32768, 4096, 2048
+    x = synth.make_aa_batch(B, T, N // 2, seed=4, device=dev)
+    n_out = T - N + 1
+    outs = [torch.empty((B, n_out), dtype=dt, device=dev)
+            for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    L_ = _lib.lib()
+
+    fused = os.environ.get("OFS_CFG4_SEPARATE", "0") != "1"
+
+    def step():
+        if fused:
+            chk(L_.ofs_sc_minn_metric(_lib.C64, x.data_ptr(), B, 1, T, N, _lib.FP32,
+                                      *[t.data_ptr() for t in outs], st.cuda_stream), "sc_minn")
+            return
+        chk(L_.ofs_sc_metric(_lib.C64, x.data_ptr(), B, 1, T, N, 1, _lib.FP32, outs[0].data_ptr(),
+                             outs[1].data_ptr(), outs[2].data_ptr(), st.cuda_stream), "sc")
+        chk(L_.ofs_minn_metric(_lib.C64, x.data_ptr(), B, 1, T, N, _lib.FP32, outs[3].data_ptr(),
+                               outs[4].data_ptr(), outs[5].data_ptr(), st.cuda_stream), "minn")
+    ms = timed(step, steps, warmup, st)
+    nbytes = B * T * 8 + 2 * B * n_out * 16
+    return dict(config="cfg4", workload=f"combined_sc_min S&C + Minn, N={N}, {B} x {T} c64 per GPU, fp32",
+                kernel=("sc_minn_fast_kernel (fused, one pass)" if fused else
+                        "win_fast_kernel<COMB> + win_fast_kernel<MINN>"), samples=B * T, ms=ms,
+                alg_bytes=nbytes, bytes_per_sample="8 in (once) + 2 x (M 4 + P 8 + R 4) per output")
+
+
+def cfg5(dev, st, steps, warmup, n_seq=1 << 20):
+    """cfg5: zc_freq metric, N=4096, one window per sequence (cp=0), 1M sequences x 4096 c64."""
+    N = 4096
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn((n_seq, N), dtype=torch.complex64, device=dev, generator=g)
+    prec = int(os.environ.get("OFS_CFG5_PREC", "0"))           # 0 fp32 window FFT, 1 fp64 sliding DFT
+    out = torch.empty((n_seq, 1), dtype=torch.float32 if prec == 0 else torch.float64, device=dev)
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    idx32 = np.ascontiguousarray(idx.astype(np.int32))
+    tb = np.ascontiguousarray(t.astype(np.complex128))
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), n_seq, 1, N, N, 0, prec, 62, idx32.ctypes.data, tb.ctypes.data, e,
+            out.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_zc_freq_metric(*args), "zc_freq"), steps, warmup, st)
+    nbytes = n_seq * (N * 8 + (4 if prec == 0 else 8))
+    return dict(config="cfg5", workload=f"zc_freq 62-bin metric, N={N}, cp=0, {n_seq} sequences x {N} c64",
+                kernel="zc_win_kernel<64> (fp32 window FFT)" if prec == 0 else "zc_freq_kernel (fp64 sliding DFT)",
+                samples=n_seq * N, ms=ms, alg_bytes=nbytes,
+                bytes_per_sample="8 in + 4|8 B per sequence out")
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    for name in a.configs.split(","):
+        t0 = time.perf_counter()
+        r = CONFIGS[name](dev, st, a.steps, a.warmup)
+        gbs = r["alg_bytes"] / (r["ms"] / 1e3) / 1e9
+        r.update(value=round(r["samples"] / (r["ms"] / 1e3) / 1e6, 1), unit="Msamples/s",
+                 ms=round(r["ms"], 4), achieved_GBs=round(gbs, 1), hbm_frac=round(gbs / HBM, 4),
+                 wall_s=round(time.perf_counter() - t0, 1))
+        print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
