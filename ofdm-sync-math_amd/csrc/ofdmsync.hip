@@ -491,80 +491,145 @@ struct RtlArgs {
     int32_t detect, hyst, toff, max_ev; int32_t* n_ev; int64_t* ev; int64_t* open_start;
 };
 
-__global__ __launch_bounds__(64) void rtl_iir_kernel(RtlArgs a) {
+// Lane-per-stream form: wave 0 of a 256-thread workgroup is the WORKER — one lane per stream,
+// 64 streams — and walks its stream's samples sequentially (recursion, threshold compare and
+// gate FSM are per-lane scalar code, no idle lanes).  Waves 1-3 are LOADERS: they stage chunk
+// c+1 of the 64 streams from HBM into an LDS ring (coalesced rows: a row is one stream's RCH
+// consecutive samples) and write chunk c-1's results back while the worker runs chunk c; one
+// barrier per chunk.  With only B/64 workgroups in flight the loaders are what keeps the
+// memory system busy.
+constexpr int RCH = 64;
+constexpr int RNB = 2;                                   // LDS ring depth: loaders store c-1 then refill it with c+1
+
+struct RtlRing {
+    double c[RNB][64][RCH + 1];                          // corr_positive in, smooth out
+    double e[RNB][64][RCH + 1];                          // energy_scaled in, corr_scaled out
+    uint8_t f[RNB][64][RCH + 4];                         // above out
+};
+
+__global__ __launch_bounds__(256) void rtl_iir_kernel(RtlArgs a, int64_t B) {
 #pragma clang fp contract(off)
-    const int64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
+    __shared__ RtlRing ring;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int64_t b0 = (int64_t)blockIdx.x * 64;
+    const int nst = (int)min((int64_t)64, B - b0);         // streams of this workgroup
     const int64_t T = a.T;
-    const double* ct = a.corr_total + b * T;
-    const double* et = a.energy_total + b * T;
+    const int nch = (int)((T + RCH - 1) / RCH);
     const int64_t vstart = 3 * (int64_t)a.Q - 1;
-    const double denom = (double)(1ll << (a.shift > 0 ? a.shift : 0));
+    const double inv = ldexp(1.0, -(a.shift > 0 ? a.shift : 0));   // exact 1 / 2^shift
     const double scale = (double)(1ll << a.frac_bits);
-    double s = 0.0;
+
+    // loader helpers (waves 1-3: 192 threads sweep the 64 x RCH tile)
+    const int lt = tid - 64;
+    auto load_chunk = [&](int c) {
+        const int64_t base = (int64_t)c * RCH;
+        const int cnt = (int)min((int64_t)RCH, T - base);
+        const int buf = c % RNB;
+        constexpr int PER_T = (64 * RCH + 191) / 192;
+        double vc[PER_T], ve[PER_T];
+#pragma unroll
+        for (int i = 0; i < PER_T; ++i) {
+            const int el = lt + 192 * i, r = el / RCH, col = el % RCH;
+            const bool ok = el < 64 * RCH && r < nst && col < cnt;
+            const int64_t g = (b0 + r) * T + base + col;
+            vc[i] = ok ? a.corr_total[g] : 0.0;
+            ve[i] = ok ? a.energy_total[g] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < PER_T; ++i) {
+            const int el = lt + 192 * i, r = el / RCH, col = el % RCH;
+            if (el < 64 * RCH) {
+                ring.c[buf][r][col] = vc[i] > 0.0 ? vc[i] : 0.0;
+                ring.e[buf][r][col] = (a.thr_value == 0.0) ? 0.0 : ve[i] * a.thr_value;
+            }
+        }
+    };
+    auto store_chunk = [&](int c) {
+        const int64_t base = (int64_t)c * RCH;
+        const int cnt = (int)min((int64_t)RCH, T - base);
+        const int buf = c % RNB;
+        for (int el = lt; el < 64 * RCH; el += 192) {
+            const int r = el / RCH, col = el % RCH;
+            if (r < nst && col < cnt) {
+                const int64_t g = (b0 + r) * T + base + col;
+                if (a.smooth) a.smooth[g] = ring.c[buf][r][col];
+                if (a.corr_scaled) a.corr_scaled[g] = ring.e[buf][r][col];
+                if (a.above) a.above[g] = ring.f[buf][r][col];
+            }
+        }
+    };
+
+    // worker state (wave 0, lane = stream)
+    const int64_t b = b0 + lane;
+    double sm = 0.0;
     long long si = 0;
     bool gate_open = false;
     long long gate_start = -1, peak_index = 0;
     double peak_value = 0.0;
     int low = 0, n_ev = 0;
     const int hyst_limit = a.hyst > 0 ? a.hyst - 1 : 0;
-    int64_t* ev = a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr;
-    for (int64_t base = 0; base < T; base += 64) {
-        const int64_t n = base + lane;
-        const bool inb = n < T;
-        const double c = inb ? ct[n] : 0.0;
-        const double cp = c > 0.0 ? c : 0.0;
-        const double e = inb ? et[n] : 0.0;
-        const double es = (a.thr_value == 0.0) ? 0.0 : e * a.thr_value;
-        double my_s = 0.0;
-        const int jend = (int)min((int64_t)64, T - base);
-        for (int j = 0; j < jend; ++j) {
-            const int64_t idx = base + j;
-            const double cpj = readlane_d(cp, j);
-            const double esj = readlane_d(es, j);
-            const bool vj = idx >= vstart;
-            if (vj) {
-                if (a.smooth_mode == 0) {
-                    if (a.shift == 0) s = cpj;
-                    else s = s + (cpj - s) / denom;
-                } else {
-                    const long long ci = (long long)cpj;
-                    si = (a.shift == 0) ? ci : si + ((ci - si) >> a.shift);
-                    s = (double)si;
-                }
-            }
-            if (lane == j) my_s = s;
-            if (a.detect && vj) {
-                const bool abv = (s * scale) >= esj;
-                if (!gate_open) {
-                    if (abv) { gate_open = true; gate_start = idx; peak_value = cpj; peak_index = idx; low = 0; }
-                } else {
-                    if (cpj >= peak_value) { peak_value = cpj; peak_index = idx; }
-                    if (abv) {
-                        low = 0;
-                    } else {
-                        const bool closing = (a.hyst == 0) || (low == hyst_limit);
-                        if (!closing) low += 1;
-                        if (closing) {
-                            if (lane == 0 && n_ev < a.max_ev) {
-                                int64_t* r = ev + (int64_t)n_ev * 4;
-                                r[0] = peak_index; r[1] = peak_index + a.toff; r[2] = gate_start; r[3] = idx + 1;
+    int64_t* ev = (wave == 0 && a.ev && b < B) ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr;
+
+    if (wave > 0) load_chunk(0);
+    __syncthreads();
+    for (int c = 0; c <= nch; ++c) {
+        if (wave == 0) {
+            if (c < nch && lane < nst) {
+                const int buf = c % RNB;
+                const int64_t base = (int64_t)c * RCH;
+                const int cnt = (int)min((int64_t)RCH, T - base);
+#pragma unroll 4
+                for (int j = 0; j < cnt; ++j) {
+                    const int64_t idx = base + j;
+                    const double cpj = ring.c[buf][lane][j];
+                    const double esj = ring.e[buf][lane][j];
+                    const bool vj = idx >= vstart;
+                    if (vj) {
+                        if (a.smooth_mode == 0) {
+                            if (a.shift == 0) sm = cpj;
+                            else sm = sm + (cpj - sm) * inv;
+                        } else {
+                            const long long ci = (long long)cpj;
+                            si = (a.shift == 0) ? ci : si + ((ci - si) >> a.shift);
+                            sm = (double)si;
+                        }
+                    }
+                    const double cs = sm * scale;
+                    const bool abv = vj && (cs >= esj);
+                    ring.c[buf][lane][j] = sm;
+                    ring.e[buf][lane][j] = cs;
+                    ring.f[buf][lane][j] = (uint8_t)abv;
+                    if (a.detect && vj) {
+                        if (!gate_open) {
+                            if (abv) { gate_open = true; gate_start = idx; peak_value = cpj; peak_index = idx; low = 0; }
+                        } else {
+                            if (cpj >= peak_value) { peak_value = cpj; peak_index = idx; }
+                            if (abv) {
+                                low = 0;
+                            } else {
+                                const bool closing = (a.hyst == 0) || (low == hyst_limit);
+                                if (!closing) low += 1;
+                                if (closing) {
+                                    if (ev && n_ev < a.max_ev) {
+                                        int64_t* rr = ev + (int64_t)n_ev * 4;
+                                        rr[0] = peak_index; rr[1] = peak_index + a.toff; rr[2] = gate_start; rr[3] = idx + 1;
+                                    }
+                                    n_ev += 1;
+                                    gate_open = false; gate_start = -1; peak_value = 0.0; low = 0;
+                                }
                             }
-                            n_ev += 1;
-                            gate_open = false; gate_start = -1; peak_value = 0.0; low = 0;
                         }
                     }
                 }
             }
+        } else {
+            if (c >= 1) store_chunk(c - 1);
+            if (c + 1 < nch) load_chunk(c + 1);
         }
-        if (inb) {
-            if (a.smooth) a.smooth[b * T + n] = my_s;
-            const double cs = my_s * scale;
-            if (a.corr_scaled) a.corr_scaled[b * T + n] = cs;
-            if (a.above) a.above[b * T + n] = (n >= vstart) && (cs >= es);
-        }
+        __syncthreads();
     }
-    if (lane == 0 && a.detect) {
+    if (wave == 0 && a.detect && b < B) {
         a.n_ev[b] = n_ev;
         if (a.open_start) a.open_start[b] = gate_open ? gate_start : -1;
     }
@@ -887,7 +952,7 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
         r.thr_value = (double)threshold_value; r.detect = detect; r.hyst = hysteresis;
         r.toff = timing_offset; r.max_ev = max_events; r.n_ev = n_events; r.ev = events;
         r.open_start = open_gate_start;
-        hipLaunchKernelGGL(rtl_iir_kernel, dim3((unsigned)B), dim3(64), 0, st, r);
+        hipLaunchKernelGGL(rtl_iir_kernel, dim3((unsigned)((B + 63) / 64)), dim3(256), 0, st, r, B);
         if (hipGetLastError() != hipSuccess) return OFS_EHIP;
     }
     return OFS_OK;
