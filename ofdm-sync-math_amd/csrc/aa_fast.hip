@@ -37,6 +37,30 @@ constexpr int FAST_WG = 256;      // 4 waves = 4 independent streams per workgro
 #define OFS_FAST_BOUNDS __launch_bounds__(FAST_WG)
 #endif
 constexpr int TMAX = 1024;        // stream length handled by the fast path
+
+// cache policy knobs (tuning builds): non-temporal output stores, LDS-DMA aux bits
+#ifndef OFS_STORE_NT
+#define OFS_STORE_NT 0
+#endif
+#ifndef OFS_DMA_AUX
+#define OFS_DMA_AUX 0
+#endif
+typedef float nf4 __attribute__((ext_vector_type(4)));
+typedef float nf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_out(float4* p, float4 v) {
+#if OFS_STORE_NT
+    __builtin_nontemporal_store(nf4{v.x, v.y, v.z, v.w}, reinterpret_cast<nf4*>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_out(float2* p, float2 v) {
+#if OFS_STORE_NT
+    __builtin_nontemporal_store(nf2{v.x, v.y}, reinterpret_cast<nf2*>(p));
+#else
+    *p = v;
+#endif
+}
 constexpr int NOKEY = 1 << 20;
 
 
@@ -67,7 +91,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                 n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
                 __builtin_amdgcn_global_load_lds((const void*)(xs + n),
                                                  (__attribute__((address_space(3))) void*)&lds[w][k * V4 + j][0],
-                                                 16, 0, 0);
+                                                 16, 0, OFS_DMA_AUX);
             }
     }
     auto xrow = [&](int k, float (&re)[E], float (&im)[E]) {
@@ -168,19 +192,19 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 #pragma unroll
             for (int j = 0; j < V4; ++j) {
                 if (nb + 2 * j < T) {
-                    if (Pout) *reinterpret_cast<float4*>(Pout + 2 * (o + 2 * j)) =
-                        make_float4(pf[2 * j][0], pf[2 * j][1], pf[2 * j + 1][0], pf[2 * j + 1][1]);
+                    if (Pout) st_out(reinterpret_cast<float4*>(Pout + 2 * (o + 2 * j)),
+                                    make_float4(pf[2 * j][0], pf[2 * j][1], pf[2 * j + 1][0], pf[2 * j + 1][1]));
                     // float4 R/M stores need T % 4 == 0: otherwise the last pair of a stream
                     // would spill into the next stream's first samples (and b*T+nb is not
                     // 16-byte aligned for odd b)
                     if (E % 4 != 0 || (T & 3) != 0) {
-                        if (Rout) *reinterpret_cast<float2*>(Rout + o + 2 * j) = make_float2(rf[2 * j], rf[2 * j + 1]);
-                        if (Mout) *reinterpret_cast<float2*>(Mout + o + 2 * j) = make_float2(mf[2 * j], mf[2 * j + 1]);
+                        if (Rout) st_out(reinterpret_cast<float2*>(Rout + o + 2 * j), make_float2(rf[2 * j], rf[2 * j + 1]));
+                        if (Mout) st_out(reinterpret_cast<float2*>(Mout + o + 2 * j), make_float2(mf[2 * j], mf[2 * j + 1]));
                     } else if ((j & 1) == 0) {
-                        if (Rout) *reinterpret_cast<float4*>(Rout + o + 2 * j) =
-                            make_float4(rf[2 * j], rf[2 * j + 1], rf[2 * j + 2], rf[2 * j + 3]);
-                        if (Mout) *reinterpret_cast<float4*>(Mout + o + 2 * j) =
-                            make_float4(mf[2 * j], mf[2 * j + 1], mf[2 * j + 2], mf[2 * j + 3]);
+                        if (Rout) st_out(reinterpret_cast<float4*>(Rout + o + 2 * j),
+                                        make_float4(rf[2 * j], rf[2 * j + 1], rf[2 * j + 2], rf[2 * j + 3]));
+                        if (Mout) st_out(reinterpret_cast<float4*>(Mout + o + 2 * j),
+                                        make_float4(mf[2 * j], mf[2 * j + 1], mf[2 * j + 2], mf[2 * j + 3]));
                     }
                     if (a.valid) { a.valid[o + 2 * j] = (k >= MR); a.valid[o + 2 * j + 1] = (k >= MR); }
                 }
