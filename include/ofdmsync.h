@@ -198,7 +198,9 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
                            int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
                            const int32_t* bin_indices, const double* template_bins,
                            double template_energy, void* metric, void* stream);
-/* which zc_freq kernel a shape runs on: 1 sliding DFT (fp64), 2 window FFT (fp32), 0 none */
+/* which zc_freq kernel a shape runs on: 1 sliding DFT (fp64), 2 window FFT (fp32), 3 N = 4096
+ * window FFT with the column sums reduced across lanes (fp32; taken when the template bins'
+ * residues mod 64 are distinct, as the PSS template's are, otherwise 2), 0 none */
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp);
 
 /*

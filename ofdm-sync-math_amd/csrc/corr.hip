@@ -491,6 +491,177 @@ __global__ __launch_bounds__(64 * ZW_WAVES) void zc_win_kernel(ZfArgs a, int nb)
 }
 
 // ------------------------------------------------------------------------------------------
+// zc_freq, N = 4096 (cfg5), fp32, no LDS transpose.  Same 64 x 64 split as zc_win_kernel
+// (lane c owns column c, a 64-point FFT in registers gives Y_c[r]), but the column sums
+// X[k] = Σ_c w_N^{kc} Y_c[k mod 64] are done ACROSS LANES: each lane scales its Y_c[r] by the
+// twiddle of the bin living at residue r (table in LDS, built once per workgroup), then a
+// reduce-scatter over the 64 lanes (permlane32/16 swaps, then DPP / swizzle xor steps) leaves
+// lane j with X of the bin at residue j.  Needs the bins' residues mod 64 distinct (the PSS
+// template's ±1..±31 are).  LDS holds only the 32 KiB table per workgroup, so occupancy is set
+// by registers (the 64-sample column), and a persistent grid keeps loads of some waves in
+// flight while others compute.
+// ------------------------------------------------------------------------------------------
+struct Zw64Args {
+    const void* x; int64_t B, T; int cp; int64_t noff; double t_energy; float* metric;
+    int kres[64];                 // bin k (mod N) whose residue k mod 64 is r, -1 if none
+    double rtr[64], rti[64];      // template value of that bin
+};
+constexpr int Z64_WAVES = 4;
+
+__device__ __forceinline__ float f_of(unsigned u) { return __uint_as_float(u); }
+__device__ __forceinline__ unsigned u_of(float f) { return __float_as_uint(f); }
+
+// v[i] += v[i + 32] of the partner half; afterwards v[i] in lane l stands for residue i + 32·l[5]
+template <int M>
+__device__ __forceinline__ void rs_swap_step(float (&v)[64]) {
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        if constexpr (M == 32) {
+            const auto p = __builtin_amdgcn_permlane32_swap(u_of(v[i]), u_of(v[i + M]), false, false);
+            v[i] = f_of(p[0]) + f_of(p[1]);
+        } else {
+            const auto p = __builtin_amdgcn_permlane16_swap(u_of(v[i]), u_of(v[i + M]), false, false);
+            v[i] = f_of(p[0]) + f_of(p[1]);
+        }
+    }
+}
+// xor-partner step for M = 8, 4, 2, 1 (within 16-lane rows)
+template <int M>
+__device__ __forceinline__ float xor_lane(float s) {
+    if constexpr (M == 8) return f_of(__builtin_amdgcn_mov_dpp(u_of(s), 0x128, 0xf, 0xf, false));  // row_ror:8
+    if constexpr (M == 2) return f_of(__builtin_amdgcn_mov_dpp(u_of(s), 0x4E, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+    if constexpr (M == 1) return f_of(__builtin_amdgcn_mov_dpp(u_of(s), 0xB1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+    return f_of(__builtin_amdgcn_ds_swizzle(u_of(s), 0x1F | (M << 10)));                           // xor 4
+}
+template <int M>
+__device__ __forceinline__ void rs_xor_step(float (&v)[64], int lane) {
+    const bool hi = (lane & M) != 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const float send = hi ? v[i] : v[i + M];
+        const float keep = hi ? v[i + M] : v[i];
+        v[i] = keep + xor_lane<M>(send);
+    }
+}
+__device__ __forceinline__ void reduce_scatter64(float (&v)[64], int lane) {
+    rs_swap_step<32>(v);
+    rs_swap_step<16>(v);
+    rs_xor_step<8>(v, lane);
+    rs_xor_step<4>(v, lane);
+    rs_xor_step<2>(v, lane);
+    rs_xor_step<1>(v, lane);
+}
+
+// LDS: twiddle table [64 residues][64 columns] + one 32 KiB window slot per wave
+constexpr size_t Z64_LDS = (size_t)64 * 64 * sizeof(float2) * (1 + Z64_WAVES);
+
+// One wave per SIMD (the 64-sample column is 128 VGPRs and the register FFT wants more): what
+// keeps HBM busy is the wave's LDS-DMA prefetch of its NEXT window, issued as soon as the current
+// window has been read out of its slot, so the load of window i+1 overlaps the FFT of window i.
+// Windows that do not start on a 16-byte boundary (odd offsets) are loaded directly instead.
+__global__ __launch_bounds__(64 * Z64_WAVES, 1) void zc_win64_kernel(Zw64Args a, int nb) {
+    constexpr int N = 4096;
+    extern __shared__ __attribute__((aligned(16))) float2 zsm[];
+    float2 (*tw)[64] = reinterpret_cast<float2 (*)[64]>(zsm);   // [residue][column] = w_N^{k(r) c}
+    for (int e = threadIdx.x; e < 64 * 64; e += 64 * Z64_WAVES) {
+        const int r = e >> 6, c = e & 63;
+        const int k = a.kres[r];
+        float2 v = make_float2(0.f, 0.f);
+        if (k >= 0) {
+            double s, co;
+            sincospi(-2.0 * (double)(((int64_t)k * c) % N) / (double)N, &s, &co);
+            v = make_float2((float)co, (float)s);
+        }
+        tw[r][c] = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float2* slot = zsm + 64 * 64 * (1 + wave);                  // this wave's window slot
+    const double tr = a.rtr[lane], ti = a.rti[lane];
+    const double emask = a.kres[lane] >= 0 ? 1.0 : 0.0;
+    const int64_t items = a.B * a.noff;
+    const int64_t stride = (int64_t)gridDim.x * Z64_WAVES;
+    // unit = (item, branch): the wave walks its units in order and prefetches the next one
+    auto window = [&](int64_t it, int br) {
+        const int64_t b = it / a.noff, o = it - b * a.noff;
+        return reinterpret_cast<const float2*>(a.x) + (b * nb + br) * a.T + o + a.cp;
+    };
+    auto aligned = [](const float2* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    auto dma = [&](const float2* xs) {                          // 32 x 1 KiB, linear copy
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(xs + 128 * j + 2 * lane),
+                                             (__attribute__((address_space(3))) void*)(slot + 128 * j),
+                                             16, 0, 0);
+    };
+    int64_t item = (int64_t)blockIdx.x * Z64_WAVES + wave;
+    int br = 0;
+    bool staged = false;                                        // current unit sits in the slot
+    if (item < items) {
+        const float2* xs = window(item, 0);
+        staged = aligned(xs);
+        if (staged) dma(xs);
+    }
+    double cr = 0.0, ci = 0.0, e = 0.0;
+    while (item < items) {
+        int64_t nitem = item;
+        int nbr = br + 1;
+        if (nbr == nb) { nbr = 0; nitem = item + stride; }
+        float re[64], im[64];
+        if (staged) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this unit's DMA has landed
+#pragma unroll
+            for (int q = 0; q < 64; ++q) {                      // column `lane`: x[64 q + lane]
+                const float2 v = slot[64 * q + lane];
+                re[q] = v.x; im[q] = v.y;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // slot read out: free to refill
+        } else {
+            const float2* xs = window(item, br);
+#pragma unroll
+            for (int q = 0; q < 64; ++q) {
+                const float2 v = xs[64 * q + lane];
+                re[q] = v.x; im[q] = v.y;
+            }
+        }
+        staged = false;
+        if (nitem < items) {                                    // prefetch the next unit
+            const float2* xs = window(nitem, nbr);
+            staged = aligned(xs);
+            if (staged) dma(xs);
+        }
+        fft_reg<64>(re, im);                                    // Y_c[r], r = 0..63
+#pragma unroll
+        for (int r = 0; r < 64; ++r) {
+            const float2 w = tw[r][lane];
+            const float yr = re[r] * w.x - im[r] * w.y;
+            const float yi = re[r] * w.y + im[r] * w.x;
+            re[r] = yr; im[r] = yi;
+        }
+        reduce_scatter64(re, lane);
+        reduce_scatter64(im, lane);
+        const double xr = re[0], xi = im[0];                    // X of the bin at residue `lane`
+        cr += tr * xr + ti * xi;                                // conj(t) * X
+        ci += tr * xi - ti * xr;
+        e += emask * (xr * xr + xi * xi);
+        if (nbr == 0) {                                         // all branches of `item` summed
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                cr += __shfl_xor(cr, off, 64);
+                ci += __shfl_xor(ci, off, 64);
+                e += __shfl_xor(e, off, 64);
+            }
+            if (lane == 0) {
+                const double den = a.t_energy * e;
+                a.metric[item] = (float)((cr * cr + ci * ci) / (den > 1e-12 ? den : 1e-12));
+            }
+            cr = 0.0; ci = 0.0; e = 0.0;
+        }
+        item = nitem; br = nbr;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // zc_v2 CFAR + gate (zc_v2.py:300-446), one wave per stream, sequential in sample order
 // (the running sum is the reference's exact left-to-right float64 recursion, so given the
 // same corr_mag the flags and local sums are bit-identical).  gate_only: use caller's
@@ -643,6 +814,39 @@ static int zw_launch(const ZfArgs& a, int nb, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
 
+// N = 4096 lane-reduce kernel: residue table (false if two bins share a residue mod 64)
+static bool zw64_args(const ZfArgs& a, Zw64Args& z) {
+    z.x = a.x; z.B = a.B; z.T = a.T; z.cp = a.cp; z.noff = a.noff; z.t_energy = a.t_energy;
+    z.metric = static_cast<float*>(a.metric);
+    for (int r = 0; r < 64; ++r) { z.kres[r] = -1; z.rtr[r] = 0.0; z.rti[r] = 0.0; }
+    for (int i = 0; i < a.nbins; ++i) {
+        const int r = a.kb[i] & 63;
+        if (z.kres[r] >= 0) return false;
+        z.kres[r] = a.kb[i]; z.rtr[r] = a.tr[i]; z.rti[r] = a.ti[i];
+    }
+    return true;
+}
+static bool zw64_enabled() {            // OFS_ZW64=0 forces zc_win_kernel (A/B timing)
+    const char* s = getenv("OFS_ZW64");
+    return !(s && s[0] == '0');
+}
+static int zw64_launch(const Zw64Args& z, int nb, hipStream_t st) {
+    const int rc = set_lds(zc_win64_kernel, Z64_LDS);
+    if (rc) return rc;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return OFS_EHIP;
+    // persistent grid: one 160 KiB workgroup per CU (OFS_ZW64_GRID overrides, for tuning)
+    const int64_t items = z.B * z.noff;
+    int64_t grid = (items + Z64_WAVES - 1) / Z64_WAVES;
+    const char* g = getenv("OFS_ZW64_GRID");
+    const int64_t cap = g ? atoll(g) : cus;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(zc_win64_kernel, dim3((unsigned)grid), dim3(64 * Z64_WAVES), Z64_LDS, st, z, nb);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
 // the window-FFT kernel serves fp32 calls with few offsets per stream (cfg5 shape)
 static bool zw_ok(int in_fmt, int precision, int N, int64_t noff) {
     const int R = N / 64;
@@ -737,6 +941,8 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
     hipStream_t st = (hipStream_t)stream;
     if (precision == OFS_FP32) {
         if (!zw_ok(in_fmt, precision, N, noff)) return OFS_EINVAL;
+        Zw64Args z;
+        if (N == 4096 && zw64_args(a, z) && zw64_enabled()) return zw64_launch(z, n_br, st);
         return zw_launch(a, n_br, st);
     }
     if (n_br > 4) return OFS_EINVAL;
@@ -754,7 +960,10 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp) {
     const int64_t noff = T - ((int64_t)N + cp) + 1;
     if (noff <= 0) return 0;
-    if (precision == OFS_FP32) return zw_ok(in_fmt, precision, N, noff) ? 2 : 0;
+    if (precision == OFS_FP32) {
+        if (!zw_ok(in_fmt, precision, N, noff)) return 0;
+        return (N == 4096 && zw64_enabled()) ? 3 : 2;
+    }
     return 1;
 }
 

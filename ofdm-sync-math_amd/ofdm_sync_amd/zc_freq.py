@@ -51,7 +51,7 @@ def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, templat
         raise ValueError("Received stream is shorter than a single OFDM symbol.")
     L = _lib.lib()
     prec = _lib.resolve_precision(batch, precision)
-    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) != 2:
+    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) not in (2, 3):
         if precision is not None:
             raise ValueError("fp32 zc_freq needs complex64 input, N = 64*2^j <= 4096 and <= 64 "
                              "offsets per stream (the window-FFT kernel); use precision='fp64'")

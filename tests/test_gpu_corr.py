@@ -254,7 +254,7 @@ def test_zc_freq_fp32_window_fft_vs_oracle(N, cp, T, nb):
     """cfg5 shape (few windows per sequence, complex64): the fp32 window-FFT kernel.
     Tolerance: metric (a ratio in [0, 1]) within 2e-5 absolute."""
     from ofdm_sync_amd import _lib
-    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 2
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == (3 if N == 4096 else 2)
     rng = np.random.default_rng(N + nb)
     B = 40
     x = rng_c(rng, B, nb, T)
@@ -270,6 +270,35 @@ def test_zc_freq_fp32_window_fft_vs_oracle(N, cp, T, nb):
         mo = O.zc_freq_metric(x[b].astype(np.complex128), N, cp, idx, t, e)
         np.testing.assert_allclose(mm[b], mo, rtol=0, atol=2e-5)
     assert mm.max() > 0.5                          # the PSS windows light up
+
+
+@pytest.mark.parametrize("B,nb,cp,T", [(1500, 1, 0, 4096), (300, 2, 1, 4099), (70, 3, 6, 4110)])
+def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, monkeypatch):
+    """N = 4096 lane-reduce kernel (plan 3): persistent grid (B*noff > resident waves), multiple
+    branches, odd window starts (direct-load fallback next to the LDS-DMA prefetch).  Against the
+    oracle on sampled streams and against the transpose kernel (plan 2) on all of them; metric
+    within 2e-5 absolute."""
+    from ofdm_sync_amd import _lib
+    N = 4096
+    rng = np.random.default_rng(B + nb)
+    x = rng_c(rng, B, nb, T)
+    sym = O.pss_symbol(N)
+    for b in range(0, B, 4):
+        o = b % (T - N - cp + 1)
+        x[b, :, cp + o:cp + o + N] += rng.uniform(0.5, 8.0) * sym
+    x = x.astype(np.complex64)
+    idx, t, e = O.zc_template()
+    xd = torch.from_numpy(x).cuda()
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 3
+    m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp).cpu().numpy()
+    monkeypatch.setenv("OFS_ZW64", "0")
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 2
+    m2 = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp).cpu().numpy()
+    np.testing.assert_allclose(m, m2, rtol=0, atol=2e-5)
+    for b in range(0, B, max(1, B // 25)):
+        mo = O.zc_freq_metric(x[b].astype(np.complex128), N, cp, idx, t, e)
+        np.testing.assert_allclose(m[b], mo, rtol=0, atol=2e-5)
+    assert m.max() > 0.5
 
 
 def test_zc_freq_fp32_unsupported_shape_raises():

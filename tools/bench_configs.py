@@ -139,8 +139,11 @@ def cfg5(dev, st, steps, warmup, n_seq=1 << 20):
             out.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_zc_freq_metric(*args), "zc_freq"), steps, warmup, st)
     nbytes = n_seq * (N * 8 + (4 if prec == 0 else 8))
+    plan = L_.ofs_zc_freq_plan(_lib.C64, prec, N, N, 0)
+    kernel = {1: "zc_freq_kernel (fp64 sliding DFT)", 2: "zc_win_kernel<64> (fp32 window FFT, LDS transpose)",
+              3: "zc_win64_kernel (fp32 window FFT, lane reduce-scatter, LDS-DMA prefetch)"}.get(plan, str(plan))
     return dict(config="cfg5", workload=f"zc_freq 62-bin metric, N={N}, cp=0, {n_seq} sequences x {N} c64",
-                kernel="zc_win_kernel<64> (fp32 window FFT)" if prec == 0 else "zc_freq_kernel (fp64 sliding DFT)",
+                kernel=kernel,
                 samples=n_seq * N, ms=ms, alg_bytes=nbytes,
                 bytes_per_sample="8 in + 4|8 B per sequence out")
 

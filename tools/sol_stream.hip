@@ -1,0 +1,132 @@
+// sol_stream.hip — speed-of-light probe for the headline kernel's memory pattern.
+//
+// The fused S&C kernel reads 8 B (complex64 x) and writes 16 B (complex64 P, f32 R, f32 M) per
+// sample over 65536 streams x 1024 samples.  This program times kernels that move exactly those
+// bytes with trivial arithmetic, so the headline's roofline fraction can be read against what
+// the chip actually sustains for a 1:2 read:write stream (and against a plain float4 copy,
+// the 6.3 TB/s figure of MI355X_MICROARCH.md).
+//
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/sol_stream tools/sol_stream.hip
+//   tools/bin/sol_stream [B] [iters]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+// float4 copy, grid-stride
+__global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, int64_t n4) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = a[i];
+}
+
+// the headline pattern, flat: a thread handles 4 consecutive samples
+__global__ void pattern_flat(const float4* __restrict__ x, float4* __restrict__ P, float4* __restrict__ R,
+                             float4* __restrict__ M, int64_t nq) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = x[2 * q], c = x[2 * q + 1];
+        P[2 * q] = a; P[2 * q + 1] = c;
+        const float4 r = make_float4(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w, c.x * c.x + c.y * c.y,
+                                     c.z * c.z + c.w * c.w);
+        R[q] = r;
+        M[q] = make_float4(r.x * 0.5f, r.y * 0.5f, r.z * 0.5f, r.w * 0.5f);
+    }
+}
+
+// the headline pattern, one wave per stream (the aa_fast geometry: 4 waves per 256-thread
+// workgroup, lane owns 4 consecutive samples of each 256-sample row); all loads first
+template <int T>
+__global__ __launch_bounds__(256) void pattern_wave(const float4* __restrict__ x, float4* __restrict__ P,
+                                                    float4* __restrict__ R, float4* __restrict__ M, int64_t B) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= B) return;
+    constexpr int RW = T / 256;
+    float4 v[RW][2];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const int64_t q = (b * T + 256 * k + 4 * lane) / 2;
+        v[k][0] = x[q]; v[k][1] = x[q + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const int64_t s = b * T + 256 * k + 4 * lane;
+        P[s / 2] = v[k][0]; P[s / 2 + 1] = v[k][1];
+        const float4 a = v[k][0], c = v[k][1];
+        const float4 r = make_float4(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w, c.x * c.x + c.y * c.y,
+                                     c.z * c.z + c.w * c.w);
+        R[s / 4] = r;
+        M[s / 4] = make_float4(r.x * 0.5f, r.y * 0.5f, r.z * 0.5f, r.w * 0.5f);
+    }
+}
+
+// read-only and write-only streams
+__global__ void read4(const float4* __restrict__ a, float* out, int64_t n4) {
+    float s = 0.f;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 v = a[i];
+        s += v.x + v.y + v.z + v.w;
+    }
+    if (s == 12345.678f) out[0] = s;
+}
+__global__ void write4(float4* __restrict__ a, int64_t n4) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+        a[i] = make_float4(1.f, 2.f, 3.f, (float)i);
+}
+
+template <class F>
+static double time_ms(F f, int iters) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) f();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipGetLastError());
+    CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
+    return ms / iters;
+}
+
+int main(int argc, char** argv) {
+    const int64_t B = argc > 1 ? atoll(argv[1]) : 65536;
+    const int64_t T = 1024;
+    const int iters = argc > 2 ? atoi(argv[2]) : 20;
+    const int64_t n = B * T;
+    float4 *x, *P, *R, *M;
+    float* dummy;
+    CK(hipMalloc(&x, n * 8)); CK(hipMalloc(&P, n * 8)); CK(hipMalloc(&R, n * 4)); CK(hipMalloc(&M, n * 4));
+    CK(hipMalloc(&dummy, 64));
+    CK(hipMemset(x, 0, n * 8));
+    int dev;
+    hipDeviceProp_t pr;
+    CK(hipGetDevice(&dev)); CK(hipGetDeviceProperties(&pr, dev));
+    const int cus = pr.multiProcessorCount;
+    printf("{\"device\": \"%s\", \"cus\": %d, \"B\": %ld, \"T\": %ld}\n", pr.gcnArchName, cus, (long)B, (long)T);
+    auto report = [&](const char* name, double bytes, double ms) {
+        printf("{\"probe\": \"%s\", \"ms\": %.5f, \"GBs\": %.1f, \"frac_8TBs\": %.4f}\n", name, ms, bytes / ms / 1e6,
+               bytes / ms / 1e6 / 8000.0);
+    };
+    const int64_t n4 = n * 8 / 16;
+    char nm[96];
+    for (int grid_mult : {4, 8, 16}) {
+        const int grid = cus * grid_mult;
+        snprintf(nm, sizeof nm, "copy4 grid=%dxCU", grid_mult);
+        report(nm, 2.0 * n * 8, time_ms([&] { copy4<<<grid, 256>>>(x, P, n4); }, iters));
+        snprintf(nm, sizeof nm, "read4 grid=%dxCU", grid_mult);
+        report(nm, 1.0 * n * 8, time_ms([&] { read4<<<grid, 256>>>(x, dummy, n4); }, iters));
+        snprintf(nm, sizeof nm, "write4 grid=%dxCU", grid_mult);
+        report(nm, 1.0 * n * 8, time_ms([&] { write4<<<grid, 256>>>(P, n4); }, iters));
+        snprintf(nm, sizeof nm, "pattern_flat(8r+16w) grid=%dxCU", grid_mult);
+        report(nm, 24.0 * n, time_ms([&] { pattern_flat<<<grid, 256>>>(x, P, R, M, n / 4); }, iters));
+    }
+    report("pattern_flat(8r+16w) grid=full", 24.0 * n,
+           time_ms([&] { pattern_flat<<<(unsigned)((n / 4 + 255) / 256), 256>>>(x, P, R, M, n / 4); }, iters));
+    report("pattern_wave(8r+16w) wave-per-stream", 24.0 * n,
+           time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    return 0;
+}
