@@ -73,6 +73,8 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
  * Which kernel ofs_aa_detect dispatches a shape to (pure query, no launch):
  *   1000 + 10*E + MR : register-resident wave-per-stream fast path (E samples per lane,
  *                      L = 64*E*MR), complex64 / OFS_FP32 / one antenna / even T <= 1024;
+ *   2000 + 10*E + MR : integer-exact wave-per-stream path, OFS_CI16 / OFS_FP64, 1-2 antennas,
+ *                      T * n_ant <= 2^21 (all window sums exact integers), L = 64*E*MR, MR <= 8;
  *   1                : general LDS engine, events fused (stream fits one tile);
  *   2                : general LDS engine, tiled, events in a second pass over P/M;
  *   <0               : invalid arguments or window too long (as ofs_aa_detect would return).
@@ -118,6 +120,14 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
                      int32_t detect, int32_t hysteresis, int32_t timing_offset,
                      int32_t max_events, int32_t* n_events, int64_t* events,
                      int64_t* open_gate_start, void* stream);
+
+/*
+ * Which kernel ofs_minn_rtl dispatches a shape to (pure query): 2000 + 10*E + MW for the
+ * integer-exact wave-per-stream kernel (OFS_CI16, 1-4 branches, T * n_br <= 2^21, Q = 64*E*MW
+ * <= 512: metric, smoothing, threshold and gate FSM in one pass), 0 for the general engine
+ * (window kernel + lane-per-stream IIR/gate kernel).
+ */
+int32_t ofs_rtl_plan(int32_t in_fmt, int32_t n_br, int64_t T, int32_t Q);
 
 /*
  * Gate / peak FSM alone on precomputed metric arrays: replaces minn_rtl.detect_minn_rtl

@@ -1,0 +1,486 @@
+// aa_exact.hip — integer-exact wave-per-stream kernels for int16 I/Q input (OFS_CI16: 12-bit ADC
+// words, the RTL's sample format, ref/minn_preamble_detector.sv:61-67):
+//
+//   aa_exact_kernel  [A][A] S&C detector: P, R, M, valid + gate / peak / CFO events
+//                    (sync_aa.py:421-571), fp64 outputs;
+//   rtl_exact_kernel RTL Minn metric (minn_rtl.py:583-733) fused with the IIR smoothing,
+//                    threshold and gate FSM (minn_rtl.py:706-722, :750-825).
+//
+// Every product and window sum of integer samples is an integer below 2^53 (checked on the
+// host: T·n_branch <= 2^21), so fp64 PREFIX DIFFERENCES ARE EXACT: any summation order gives the
+// bits of the reference's sequential running sums.  No cancellation-free split is needed
+// (contrast aa_fast.hip), which makes this the cheap path: one wave per stream, rows of
+// RL = 64·E samples (lane l owns samples RL·k + E·l + e), the lagged sample and the lagged
+// prefix values sit in the same lane and element a whole number of rows back.
+//
+// The RTL smoothing s += (c - s) / 2^k is the reference's float64 recursion and is sequential in
+// time; it runs inside the same wave, row by row, on wave-uniform values (v_readlane of the
+// row's corr_positive), so the metric never makes a round trip through HBM before smoothing.
+#include "ofs_common.h"
+#include "aa_gate.h"
+#include "ofdmsync.h"
+
+using namespace ofs;
+
+namespace {
+
+constexpr int XW = 256;                 // 4 waves = 4 streams per workgroup
+
+// E consecutive int16 I/Q words (packed (I, Q) in one int32) of one lane, zero past T
+template <int E>
+__device__ __forceinline__ void load_words(const int32_t* xs, int64_t n0, int64_t T, int32_t (&w)[E]) {
+    if (n0 + E <= T && (reinterpret_cast<uintptr_t>(xs + n0) & (4 * E - 1)) == 0) {
+        if constexpr (E == 1) {
+            w[0] = xs[n0];
+        } else if constexpr (E == 2) {
+            const int2 v = *reinterpret_cast<const int2*>(xs + n0);
+            w[0] = v.x; w[1] = v.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < E; j += 4) {
+                const int4 v = *reinterpret_cast<const int4*>(xs + n0 + j);
+                w[j] = v.x; w[j + 1] = v.y; w[j + 2] = v.z; w[j + 3] = v.w;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) w[e] = (n0 + e < T) ? xs[n0 + e] : 0;
+    }
+}
+__device__ __forceinline__ double w_re(int32_t w) { return (double)(int16_t)(w & 0xffff); }
+__device__ __forceinline__ double w_im(int32_t w) { return (double)(w >> 16); }
+
+// in-lane inclusive prefix of v, then the lane's exclusive wave prefix and the row total
+template <int E>
+struct RowPrefix {
+    double f[E], excl, tot;
+    __device__ __forceinline__ void run(const double (&v)[E]) {
+        f[0] = v[0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) f[e] = f[e - 1] + v[e];
+        const double incl = scan_add(f[E - 1]);
+        excl = shr1z(incl);
+        tot = readlane(incl, 63);
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// sync_aa, integer input.  P[n] = A(n) - A(n-L), R[n] = Ae(n) - Ae(n-L) with A the prefix of
+// x[j]·conj(x[j-L]) (0 while the delay line fills) and Ae that of |x[j]|², summed over antennas;
+// valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
+// ------------------------------------------------------------------------------------------
+template <int E, int MR, int NA>
+__global__ __launch_bounds__(XW) void aa_exact_kernel(AaFastArgs a) {
+    constexpr int RL = 64 * E;
+    constexpr int L = MR * RL;
+    constexpr int PD = E <= 2 ? 4 : 2;                       // rows in flight ahead of use
+    constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * (XW / 64) + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int nrows = (int)((T + RL - 1) / RL);
+    const int32_t* xs = reinterpret_cast<const int32_t*>(a.x) + b * NA * T;
+
+    int32_t lag[NA][MR][E];                                  // raw words of rows k-MR..k-1
+    double Ar[MR][E], Ai[MR][E], Ae[MR][E];                  // prefix values of rows k-MR..k-1
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            Ar[m][e] = 0.0; Ai[m][e] = 0.0; Ae[m][e] = 0.0;
+#pragma unroll
+            for (int t = 0; t < NA; ++t) lag[t][m][e] = 0;
+        }
+    double CR = 0.0, CI = 0.0, CE = 0.0;                     // prefix at the start of row k
+
+    int32_t nx[PD][NA][E];
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+        for (int t = 0; t < NA; ++t) load_words<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
+
+    AaRowGate<E, double> gate;
+    if (a.detect)
+        gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
+                  a.ev_r + b * (int64_t)a.max_ev * 4);
+    double2* Pout = reinterpret_cast<double2*>(a.P) + b * T;
+    double* Rout = reinterpret_cast<double*>(a.R) + b * T;
+    double* Mout = reinterpret_cast<double*>(a.M) + b * T;
+    uint8_t* Vout = a.valid ? a.valid + b * T : nullptr;
+    const double floor_ = 1e-6 * (double)L;
+
+    for (int k0 = 0; k0 < nrows; k0 += PER) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = k0 + u;
+            if (k < nrows) {
+                const int nb = RL * k + E * lane;
+                int32_t cur[NA][E];
+#pragma unroll
+                for (int t = 0; t < NA; ++t)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) cur[t][e] = nx[u % PD][t][e];
+                if (k + PD < nrows) {
+#pragma unroll
+                    for (int t = 0; t < NA; ++t)
+                        load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[u % PD][t]);
+                }
+                const int sl = u % MR;                       // ring slot of row k-MR (and k)
+                double pr[E], pi[E], en[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    pr[e] = 0.0; pi[e] = 0.0; en[e] = 0.0;
+#pragma unroll
+                    for (int t = 0; t < NA; ++t) {
+                        const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
+                        const double dr = w_re(lag[t][sl][e]), di = w_im(lag[t][sl][e]);
+                        pr[e] += xr * dr + xi * di;                  // x[n]·conj(x[n-L]), exact
+                        pi[e] += xi * dr - xr * di;
+                        en[e] += xr * xr + xi * xi;
+                        lag[t][sl][e] = cur[t][e];
+                    }
+                }
+                RowPrefix<E> qr, qi, qe;
+                qr.run(pr); qi.run(pi); qe.run(en);
+                double oP[E][2], oR[E], oM[E], opm[E];
+                const bool valid = k >= MR;                          // n >= L for the whole row
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const double A_r = (CR + qr.excl) + qr.f[e];
+                    const double A_i = (CI + qi.excl) + qi.f[e];
+                    const double A_e = (CE + qe.excl) + qe.f[e];
+                    const double Pr = A_r - Ar[sl][e], Pi = A_i - Ai[sl][e], Rr = A_e - Ae[sl][e];
+                    Ar[sl][e] = A_r; Ai[sl][e] = A_i; Ae[sl][e] = A_e;
+                    const double pm = Pr * Pr + Pi * Pi;
+                    double m = 0.0;
+                    if (valid && Rr > floor_) { m = pm / (Rr * Rr); m = m < 1.0 ? m : 1.0; }
+                    oP[e][0] = Pr; oP[e][1] = Pi; oR[e] = Rr; oM[e] = m; opm[e] = pm;
+                }
+                CR += qr.tot; CI += qi.tot; CE += qe.tot;
+                // stores: a lane's E samples are contiguous
+                const bool whole = nb + E <= T && ((T & 1) == 0);
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (a.P && nb + e < T) Pout[nb + e] = make_double2(oP[e][0], oP[e][1]);
+                if (whole && E >= 2) {
+#pragma unroll
+                    for (int e = 0; e < E; e += 2) {
+                        if (a.R) *reinterpret_cast<double2*>(Rout + nb + e) = make_double2(oR[e], oR[e + 1]);
+                        if (a.M) *reinterpret_cast<double2*>(Mout + nb + e) = make_double2(oM[e], oM[e + 1]);
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < E; ++e)
+                        if (nb + e < T) {
+                            if (a.R) Rout[nb + e] = oR[e];
+                            if (a.M) Mout[nb + e] = oM[e];
+                        }
+                }
+                if (Vout) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e)
+                        if (nb + e < T) Vout[nb + e] = (uint8_t)valid;
+                }
+                if (a.detect && valid) {
+                    double ppr[E], ppi[E];
+#pragma unroll
+                    for (int e = 0; e < E; ++e) { ppr[e] = oP[e][0]; ppi[e] = oP[e][1]; }
+                    gate.row(lane, k, nb, (int)T, oM, opm, ppr, ppi);
+                }
+            }
+        }
+    }
+    if (a.detect) gate.finish(lane, (int)T, a.n_ev + b);
+}
+
+// ------------------------------------------------------------------------------------------
+// minn_rtl, integer input.  With Ac / Ae the prefixes of the lag-Q real product
+// Re(x[j]·conj(x[j-Q])) (0 while the delay line fills) and of |x[j]|², summed over branches,
+// and Q-windows C(i) = Ac(i) - Ac(i-Q), En(i) = Ae(i) - Ae(i-Q) (the _antenna_path registers
+// hold 0 until their first valid sample):
+//   corr_total   = [i >= Q-1] C(i) + [i >= 2Q-1] C(i-Q)
+//   energy_total = [i >= Q-1] En(i) + [i >= 2Q-1] En(i-Q) + [i >= 3Q-1] En(i-2Q)
+//   metric_valid = i >= 3Q-1                                  (minn_rtl.py:609-643, :691-702)
+// The lagged prefixes (Q, 2Q, 3Q back) live in a per-wave LDS ring of rows.
+// ------------------------------------------------------------------------------------------
+// IIR over one row: positions j < cnt of the row in order (lane j / E, element j % E); the state
+// updates from position vfrom on (metric_valid), holds before.  MODE 0: s += (c - s) / 2^k in
+// float64 (minn_rtl.py:706-715, contraction off: the reference's exact operation sequence);
+// 1: shift 0, s = c; 2: integer floor shift of the RTL (ref/minn_preamble_detector.sv:288-296).
+template <int E, int MODE>
+__device__ __forceinline__ void smooth_row(const double (&c)[E], double (&out)[E], double& sm, long long& si,
+                                           int lane, int cnt, int vfrom, double inv, int shift) {
+#pragma clang fp contract(off)
+    const int lanes = (cnt + E - 1) / E;
+    for (int l = 0; l < lanes; ++l) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int j = E * l + e;
+            if (j < cnt) {
+                if (j >= vfrom) {
+                    const double cj = readlane(c[e], l);
+                    if constexpr (MODE == 0) {
+                        sm = sm + (cj - sm) * inv;
+                    } else if constexpr (MODE == 1) {
+                        sm = cj;
+                    } else {
+                        const long long ci = (long long)cj;
+                        si = (shift == 0) ? ci : si + ((ci - si) >> shift);
+                        sm = (double)si;
+                    }
+                }
+                if (lane == l) out[e] = sm;
+            }
+        }
+    }
+}
+
+struct RtlExactArgs {
+    const void* x; int64_t B, T; int32_t nb, Q;
+    int32_t shift, smooth_mode, frac_bits; double thr_value;
+    double* corr_total; double* corr_positive; double* smooth; double* energy_total;
+    double* corr_scaled; double* energy_scaled; uint8_t* mvalid; uint8_t* above;
+    int32_t detect, hyst, toff, max_ev; int32_t* n_ev; int64_t* ev; int64_t* open_start;
+};
+
+// per-wave LDS ring: prefix rows k-3MW..k of Ae and Ac, and the raw words of rows k-MW..k-1
+// of every branch (lane-private columns: conflict-free, no barriers)
+__host__ __device__ constexpr int rtl_ring_rows(int MW) { return 3 * MW + 1; }
+__host__ __device__ constexpr size_t rtl_wave_lds(int E, int MW, int nb) {
+    return (size_t)2 * rtl_ring_rows(MW) * E * 64 * sizeof(double) + (size_t)nb * MW * E * 64 * sizeof(int32_t);
+}
+
+template <int E, int MW>
+__global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
+#pragma clang fp contract(off)
+    constexpr int RL = 64 * E;
+    constexpr int Q = MW * RL;
+    constexpr int NR = rtl_ring_rows(MW);
+    extern __shared__ __attribute__((aligned(16))) double rsm[];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int wpb = blockDim.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * wpb + w;
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int nb_ = a.nb;
+    double* hae_ = rsm + (rtl_wave_lds(E, MW, nb_) / sizeof(double)) * w;
+    double* hac_ = hae_ + NR * E * 64;
+    int32_t* hx_ = reinterpret_cast<int32_t*>(hac_ + NR * E * 64);
+    auto hae = [&](int r, int e) -> double& { return hae_[(r * E + e) * 64 + lane]; };
+    auto hac = [&](int r, int e) -> double& { return hac_[(r * E + e) * 64 + lane]; };
+    auto hx = [&](int t, int m, int e) -> int32_t& { return hx_[((t * MW + m) * E + e) * 64 + lane]; };
+    const int nrows = (int)((T + RL - 1) / RL);
+    const int32_t* xs = reinterpret_cast<const int32_t*>(a.x) + b * nb_ * T;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int e = 0; e < E; ++e) { hae(r, e) = 0.0; hac(r, e) = 0.0; }
+    for (int t = 0; t < nb_; ++t)
+#pragma unroll
+        for (int m = 0; m < MW; ++m)
+#pragma unroll
+            for (int e = 0; e < E; ++e) hx(t, m, e) = 0;
+
+    const int64_t row_off = b * T;
+    const int vstart = 3 * Q - 1;
+    const double inv = ldexp(1.0, -(a.shift > 0 ? a.shift : 0));   // exact 1 / 2^shift
+    const double scale = (double)(1ll << a.frac_bits);
+    const bool seq = a.smooth || a.corr_scaled || a.above || a.detect;
+    const int smode = a.smooth_mode == 1 ? 2 : (a.shift == 0 ? 1 : 0);
+    double CC = 0.0, CE = 0.0;
+    double sm = 0.0;                                               // IIR state (wave-uniform)
+    long long si = 0;
+    AaRowGate<E, double, true> gate;                               // detect_minn_rtl, closed form
+    if (a.detect)
+        gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
+                  nullptr, a.toff);
+
+    for (int k = 0; k < nrows; ++k) {
+        const int nb = RL * k + E * lane;
+        const int xsl = k % MW;
+        double pc[E], en[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
+        for (int t = 0; t < nb_; ++t) {
+            int32_t cur[E];
+            load_words<E>(xs + t * T, nb, T, cur);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int32_t d = hx(t, xsl, e);
+                const double xr = w_re(cur[e]), xi = w_im(cur[e]);
+                pc[e] += w_re(d) * xr + w_im(d) * xi;                // minn_rtl.py:616, exact
+                en[e] += xr * xr + xi * xi;                           // :617
+                hx(t, xsl, e) = cur[e];
+            }
+        }
+        RowPrefix<E> qc, qe;
+        qc.run(pc); qe.run(en);
+        const int s0 = k % NR;                                         // slot of row k
+        const int s1 = (k + NR - MW) % NR, s2 = (k + NR - 2 * MW) % NR, s3 = (k + NR - 3 * MW) % NR;
+        double ct[E], cpos[E], et[E], es[E];
+        bool mv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const double c0 = (CC + qc.excl) + qc.f[e];
+            const double e0 = (CE + qe.excl) + qe.f[e];
+            hac(s0, e) = c0;
+            hae(s0, e) = e0;
+            // prefixes before the stream start are 0
+            const double c1 = k >= MW ? hac(s1, e) : 0.0;
+            const double c2 = k >= 2 * MW ? hac(s2, e) : 0.0;
+            const double e1 = k >= MW ? hae(s1, e) : 0.0;
+            const double e2 = k >= 2 * MW ? hae(s2, e) : 0.0;
+            const double e3 = k >= 3 * MW ? hae(s3, e) : 0.0;
+            const int i = nb + e;
+            const double cr_ = (i >= Q - 1) ? c0 - c1 : 0.0;
+            const double cp_ = (i >= 2 * Q - 1) ? c1 - c2 : 0.0;
+            const double er_ = (i >= Q - 1) ? e0 - e1 : 0.0;
+            const double ep_ = (i >= 2 * Q - 1) ? e1 - e2 : 0.0;
+            const double ep2 = (i >= 3 * Q - 1) ? e2 - e3 : 0.0;
+            ct[e] = 0.0 + (cr_ + cp_);                                 // minn_rtl.py:696
+            et[e] = 0.0 + ((er_ + ep_) + ep2);                         // :697-701
+            cpos[e] = ct[e] > 0.0 ? ct[e] : 0.0;                       // :704
+            es[e] = (a.thr_value == 0.0) ? 0.0 : et[e] * a.thr_value;  // :718-721
+            mv[e] = i >= vstart;
+        }
+        CC += qc.tot; CE += qe.tot;
+
+        // smoothing: the reference's sequential recursion over the row's samples, in order, on
+        // wave-uniform values (only the IIR chain is serial); threshold and gate are vector work
+        double smv[E];
+        bool abv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) { smv[e] = 0.0; abv[e] = false; }
+        if (seq) {
+            const int64_t r0 = (int64_t)RL * k;
+            const int cnt = (int)min((int64_t)RL, T - r0);
+            const int vfrom = (int)max((int64_t)0, min((int64_t)cnt, (int64_t)vstart - r0));
+            if (smode == 0) smooth_row<E, 0>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
+            else if (smode == 1) smooth_row<E, 1>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
+            else smooth_row<E, 2>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                abv[e] = mv[e] && nb + e < T && (smv[e] * scale >= es[e]);   // minn_rtl.py:717-722
+            if (a.detect && r0 + cnt > vstart) {
+                double none[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) none[e] = 0.0;
+                gate.row_flags(lane, k, nb, (int)T, abv, cpos, none, none, none);
+            }
+        }
+        // stores (lane-consecutive)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int64_t i = nb + e;
+            if (i < T) {
+                const int64_t g = row_off + i;
+                a.corr_total[g] = ct[e];
+                if (a.corr_positive) a.corr_positive[g] = cpos[e];
+                a.energy_total[g] = et[e];
+                if (a.energy_scaled) a.energy_scaled[g] = es[e];
+                if (a.mvalid) a.mvalid[g] = (uint8_t)mv[e];
+                if (a.smooth) a.smooth[g] = smv[e];
+                if (a.corr_scaled) a.corr_scaled[g] = smv[e] * scale;
+                if (a.above) a.above[g] = (uint8_t)abv[e];
+            }
+        }
+    }
+    if (a.detect) gate.finish(lane, (int)T, a.n_ev + b, a.open_start ? a.open_start + b : nullptr);
+}
+
+// ---- dispatch -------------------------------------------------------------------------------
+bool exact_enabled() {                  // OFS_EXACT=0 forces the general engine (A/B, tests)
+    const char* s = getenv("OFS_EXACT");
+    return !(s && s[0] == '0');
+}
+
+template <int E, int MR, int NA>
+int aa_launch(const AaFastArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL((aa_exact_kernel<E, MR, NA>), dim3((unsigned)((a.B + 3) / 4)), dim3(XW), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
+template <int E, int MR>
+int aa_launch_na(int na, const AaFastArgs& a, hipStream_t st) {
+    switch (na) {
+        case 1: return aa_launch<E, MR, 1>(a, st);
+        case 2: return aa_launch<E, MR, 2>(a, st);
+    }
+    return 0;
+}
+template <int E>
+int aa_launch_mr(int mr, int na, const AaFastArgs& a, hipStream_t st) {
+    switch (mr) {
+        case 1: return aa_launch_na<E, 1>(na, a, st);
+        case 2: return aa_launch_na<E, 2>(na, a, st);
+        case 4: return aa_launch_na<E, 4>(na, a, st);
+        case 8: return aa_launch_na<E, 8>(na, a, st);
+    }
+    return 0;
+}
+
+template <int E, int MW>
+int rtl_launch(const RtlExactArgs& a, hipStream_t st) {
+    const size_t per_wave = rtl_wave_lds(E, MW, a.nb);
+    int wpb = 4;                                             // waves (streams) per workgroup
+    while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
+    const size_t lds = per_wave * wpb;
+    auto k = rtl_exact_kernel<E, MW>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return OFS_EHIP;
+    hipLaunchKernelGGL(k, dim3((unsigned)((a.B + wpb - 1) / wpb)), dim3(64 * wpb), lds, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
+
+}  // namespace
+
+// 10*E + MR of the exact aa kernel for a shape, 0 if not covered
+int ofs_aa_exact_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
+    if (fmt != OFS_CI16 || precision != OFS_FP64 || n_ant < 1 || n_ant > 2 || !exact_enabled()) return 0;
+    if (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2) return 0;   // sums < 2^53
+    if (L == 64) return 11;
+    if (L % 128 == 0 && (L == 128 || L == 256 || L == 512 || L == 1024)) return 20 + L / 128;
+    return 0;
+}
+
+int ofs_aa_exact_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
+    const int plan = ofs_aa_exact_plan(fmt, precision, n_ant, a.T, a.L);
+    if (!plan) return 0;
+    const int E = plan / 10, mr = plan % 10;
+    if (E == 1) return aa_launch_na<1, 1>(n_ant, a, st);
+    return aa_launch_mr<2>(mr, n_ant, a, st);
+}
+
+int ofs_rtl_exact_plan(int fmt, int n_br, int64_t T, int Q) {
+    if (fmt != OFS_CI16 || n_br < 1 || n_br > 4 || !exact_enabled()) return 0;
+    if (T < 1 || T * n_br > (1 << 21)) return 0;
+    for (int e : {1, 2, 4}) {
+        if (Q % (64 * e)) continue;
+        const int mw = Q / (64 * e);
+        if (mw == 1 || mw == 2) return 10 * e + mw;
+    }
+    return 0;                                                // Q > 512 or not a multiple of 64
+}
+
+int ofs_rtl_exact_try(int fmt, int n_br, const RtlExactCall& c, hipStream_t st) {
+    const int plan = ofs_rtl_exact_plan(fmt, n_br, c.T, c.Q);
+    if (!plan) return 0;
+    RtlExactArgs a;
+    a.x = c.x; a.B = c.B; a.T = c.T; a.nb = n_br; a.Q = c.Q;
+    a.shift = c.shift; a.smooth_mode = c.smooth_mode; a.frac_bits = c.frac_bits; a.thr_value = c.thr_value;
+    a.corr_total = c.corr_total; a.corr_positive = c.corr_positive; a.smooth = c.smooth;
+    a.energy_total = c.energy_total; a.corr_scaled = c.corr_scaled; a.energy_scaled = c.energy_scaled;
+    a.mvalid = c.mvalid; a.above = c.above; a.detect = c.detect; a.hyst = c.hyst; a.toff = c.toff;
+    a.max_ev = c.max_ev; a.n_ev = c.n_ev; a.ev = c.ev; a.open_start = c.open_start;
+    switch (plan) {
+        case 11: return rtl_launch<1, 1>(a, st);
+        case 12: return rtl_launch<1, 2>(a, st);
+        case 21: return rtl_launch<2, 1>(a, st);
+        case 22: return rtl_launch<2, 2>(a, st);
+        case 41: return rtl_launch<4, 1>(a, st);
+        case 42: return rtl_launch<4, 2>(a, st);
+    }
+    return 0;
+}

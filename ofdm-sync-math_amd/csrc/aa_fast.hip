@@ -16,9 +16,10 @@
 // the register footprint at ~3L/64 retained floats per lane.
 //
 // Gate / peak / CFO events (sync_aa.py:495-568) use the closed form of aa_events
-// (ofdmsync.hip), streamed row by row: prev-above by lane-serial + DPP max-scan,
+// (ofdmsync.hip), streamed row by row (aa_gate.h): prev-above by lane-serial + DPP max-scan,
 // opens/closes by ballot, per-gate argmax by wave reductions, scalar carry between rows.
 #include "ofs_common.h"
+#include "aa_gate.h"
 #include "ofdmsync.h"
 
 using namespace ofs;
@@ -61,7 +62,6 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
     *p = v;
 #endif
 }
-constexpr int NOKEY = 1 << 20;
 
 
 // Stream staging: the wave DMAs its whole stream into a private 8 KiB LDS slice
@@ -108,22 +108,10 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     double Cr[RW + 1], Ci[RW + 1], Ce[RW + 1];  // running row bases (wave-uniform)
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
-    // event state (wave-uniform)
-    const int Hp = a.hyst > 1 ? a.hyst : 1;
-    int carry_last = -1, n_ev = 0, ev_start = 0, gate_open = 0, bidx = 0;
-    float bpm = -1.f, bpr = 0.f, bpi = 0.f, bm = 0.f;
-    int64_t* evi = a.detect ? a.ev_i + b * (int64_t)a.max_ev * 4 : nullptr;
-    double* evr = a.detect ? a.ev_r + b * (int64_t)a.max_ev * 4 : nullptr;
-    auto emit = [&](int gate_end) {
-        if (lane == 0 && n_ev < a.max_ev) {
-            int64_t* ei = evi + (int64_t)n_ev * 4;
-            double* er = evr + (int64_t)n_ev * 4;
-            ei[0] = bidx; ei[1] = ev_start; ei[2] = gate_end; ei[3] = (int64_t)bidx - 2 * L + 1;
-            er[0] = bpr; er[1] = bpi; er[2] = bm;
-            er[3] = atan2((double)bpi, (double)bpr) * a.fs / (2.0 * M_PI * (double)L);
-        }
-        n_ev += 1;
-    };
+    AaRowGate<E, float> gate;                   // event state (wave-uniform)
+    if (a.detect)
+        gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
+                  a.ev_r + b * (int64_t)a.max_ev * 4);
 
     float* Pout = reinterpret_cast<float*>(a.P);
     float* Rout = reinterpret_cast<float*>(a.R);
@@ -210,87 +198,16 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                 }
             }
 
-            // ---- events: closed-form gate machine, streamed per row ----
+            // ---- events: closed-form gate machine, streamed per row (aa_gate.h) ----
             if (a.detect && k >= MR) {
-                bool ab[E];
-                int lane_last = -1;
+                float pr[E], pi[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    ab[e] = (nb + e < T) && (double)mf[e] >= a.thr;
-                    if (ab[e]) lane_last = nb + e;
-                }
-                const int W = max(wave_scan_max(lane_last, lane), carry_last);
-                int run = wave_shr1(W, lane, carry_last);
-                uint64_t Om[E], Cm[E];
-                uint64_t any = 0;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int n = nb + e;
-                    const int pe = run;
-                    if (ab[e]) run = n;
-                    const bool cl = (n < T) && run >= 0 && (n - run) == Hp;
-                    const bool op = ab[e] && (pe < 0 || (n - 1 - pe) >= Hp);
-                    Om[e] = __ballot(op);
-                    Cm[e] = __ballot(cl);
-                    any |= Om[e] | Cm[e];
-                }
-                carry_last = readlane(W, 63);
-
-                auto seg_reduce = [&](int lo, int hi) {        // first argmax of |P|² on keys [lo, hi]
-                    // per-lane best (strict >: lowest element wins ties), then across lanes
-                    float lv = -1.f, lpr = 0.f, lpi = 0.f, lm = 0.f;
-                    int lk = NOKEY;
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const int key = E * lane + e;
-                        const bool in = nb + e < T && key >= lo && key <= hi;
-                        if (in && pmf[e] > lv) { lv = pmf[e]; lk = key; lpr = pf[e][0]; lpi = pf[e][1]; lm = mf[e]; }
-                    }
-                    const float vmax = wave_max(lv);
-                    const int kk = wave_min(lv == vmax ? lk : NOKEY);
-                    if (vmax > bpm && kk != NOKEY) {
-                        const int ln = kk / E;
-                        bpr = readlane(lpr, ln);
-                        bpi = readlane(lpi, ln);
-                        bm = readlane(lm, ln);
-                        bpm = vmax;
-                        bidx = RL * k + kk;
-                    }
-                };
-
-                int seg_lo = gate_open ? 0 : -1;
-                if (any) {
-                    int pos = -1;
-                    while (true) {
-                        int key = NOKEY, is_open = 0;
-#pragma unroll
-                        for (int e = 0; e < E; ++e) {
-                            const int q = pos - e;
-                            const int t = q < 0 ? 0 : q / E + 1;       // lanes whose key > pos
-                            const uint64_t msk = t >= 64 ? 0ull : (~0ull << t);
-                            const uint64_t o = Om[e] & msk, c = Cm[e] & msk;
-                            if (o) { const int kq = E * __builtin_ctzll(o) + e; if (kq < key) { key = kq; is_open = 1; } }
-                            if (c) { const int kq = E * __builtin_ctzll(c) + e; if (kq < key) { key = kq; is_open = 0; } }
-                        }
-                        if (key == NOKEY) break;
-                        if (is_open) {
-                            gate_open = 1; ev_start = RL * k + key; seg_lo = key; bpm = -1.f;
-                        } else {
-                            seg_reduce(seg_lo, key);
-                            emit(RL * k + key);
-                            gate_open = 0; seg_lo = -1;
-                        }
-                        pos = key;
-                    }
-                }
-                if (gate_open) seg_reduce(seg_lo, RL - 1);
+                for (int e = 0; e < E; ++e) { pr[e] = pf[e][0]; pi[e] = pf[e][1]; }
+                gate.row(lane, k, nb, T, mf, pmf, pr, pi);
             }
         }
     }
-    if (a.detect) {
-        if (gate_open) emit(T);
-        if (lane == 0) a.n_ev[b] = n_ev;
-    }
+    if (a.detect) gate.finish(lane, T, a.n_ev + b);
 }
 
 template <int E, int MR>

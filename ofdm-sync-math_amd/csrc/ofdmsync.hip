@@ -834,7 +834,10 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
         f.x = x; f.B = B; f.T = T; f.L = L; f.P = P; f.R = R; f.M = M; f.valid = valid;
         f.detect = detect; f.thr = threshold; f.hyst = hysteresis; f.fs = sample_rate;
         f.max_ev = max_events; f.n_ev = n_events; f.ev_i = ev_int; f.ev_r = ev_real;
-        const int frc = ofs_aa_fast_try(in_fmt, precision, n_ant, f, st);
+        int frc = ofs_aa_fast_try(in_fmt, precision, n_ant, f, st);
+        if (frc == 1) return OFS_OK;
+        if (frc < 0) return frc;
+        frc = ofs_aa_exact_try(in_fmt, precision, n_ant, f, st);      // int16 I/Q, fp64 (aa_exact.hip)
         if (frc == 1) return OFS_OK;
         if (frc < 0) return frc;
     }
@@ -873,6 +876,8 @@ int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T,
     if (!fmt_ok(in_fmt) || !prec_ok(precision) || n_ant < 1 || T < 0 || L < 1) return OFS_EINVAL;
     const int fp = ofs_aa_fast_plan(in_fmt, precision, n_ant, T, L);
     if (fp) return 1000 + fp;
+    const int xp = ofs_aa_exact_plan(in_fmt, precision, n_ant, T, L);
+    if (xp) return 2000 + xp;
     if (2 * (int64_t)L - 1 > 0x3fffffff) return OFS_ETOOLONG;
     Plan p;
     const int lo = -(int)(2 * (int64_t)L - 1);
@@ -938,6 +943,19 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
     if (B == 0 || T == 0) return OFS_OK;
     if (3 * (int64_t)Q - 1 > 0x3fffffff) return OFS_ETOOLONG;
     hipStream_t st = (hipStream_t)stream;
+    {   // int16 I/Q: exact wave-per-stream kernel, metric + smoothing + gate in one pass
+        RtlExactCall c{};
+        c.x = x; c.B = B; c.T = T; c.Q = Q; c.shift = smooth_shift; c.smooth_mode = smooth_mode;
+        c.frac_bits = threshold_frac_bits; c.thr_value = (double)threshold_value;
+        c.corr_total = corr_total; c.corr_positive = corr_positive; c.smooth = smooth_metric;
+        c.energy_total = energy_total; c.corr_scaled = corr_scaled; c.energy_scaled = energy_scaled;
+        c.mvalid = metric_valid; c.above = above_threshold; c.detect = detect; c.hyst = hysteresis;
+        c.toff = timing_offset; c.max_ev = max_events; c.n_ev = n_events; c.ev = events;
+        c.open_start = open_gate_start;
+        const int frc = ofs_rtl_exact_try(in_fmt, n_br, c, st);
+        if (frc == 1) return OFS_OK;
+        if (frc < 0) return frc;
+    }
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = T; a.nb = n_br; a.Q = Q; a.D = Q; a.W = Q;
     a.corr_total = corr_total; a.corr_positive = corr_positive; a.energy_total = energy_total;
@@ -956,6 +974,11 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
         if (hipGetLastError() != hipSuccess) return OFS_EHIP;
     }
     return OFS_OK;
+}
+
+int32_t ofs_rtl_plan(int32_t in_fmt, int32_t n_br, int64_t T, int32_t Q) {
+    const int xp = ofs_rtl_exact_plan(in_fmt, n_br, T, Q);
+    return xp ? 2000 + xp : 0;
 }
 
 int32_t ofs_minn_rtl_gate(const double* corr_positive, const uint8_t* above_threshold,

@@ -68,6 +68,16 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
     return v;
 }
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
 __device__ __forceinline__ int wave_min(int v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
@@ -108,6 +118,21 @@ struct AaFastArgs {
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st);
 // 10*E + MR of the fast kernel a shape dispatches to, 0 if the general engine handles it
 int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L);
+
+// integer-exact wave-per-stream paths for int16 I/Q input (aa_exact.hip): 10*E + MR (or MW) of
+// the kernel a shape dispatches to, 0 if the general engine handles it; *_try returns 1 if
+// launched, 0 if not covered, <0 on error
+int ofs_aa_exact_plan(int fmt, int precision, int n_ant, int64_t T, int L);
+int ofs_aa_exact_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st);
+struct RtlExactCall {
+    const void* x; int64_t B, T; int32_t Q;
+    int32_t shift, smooth_mode, frac_bits; double thr_value;
+    double* corr_total; double* corr_positive; double* smooth; double* energy_total;
+    double* corr_scaled; double* energy_scaled; uint8_t* mvalid; uint8_t* above;
+    int32_t detect, hyst, toff, max_ev; int32_t* n_ev; int64_t* ev; int64_t* open_start;
+};
+int ofs_rtl_exact_plan(int fmt, int n_br, int64_t T, int Q);
+int ofs_rtl_exact_try(int fmt, int n_br, const RtlExactCall& c, hipStream_t st);
 
 // streaming fast path of the S&C / combined S&C / Minn window metrics (win_fast.hip)
 struct WinFastArgs {

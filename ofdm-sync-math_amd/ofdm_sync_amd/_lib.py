@@ -51,6 +51,7 @@ def _declare(lib):
         "ofs_sc_minn_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P,
                                          P, P, P, P, P]),
         "ofs_win_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int64, c_int32]),
+        "ofs_rtl_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32]),
         "ofs_zc_freq_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32, c_int32]),
         "ofs_zc_detect": (c_int32, [P, c_int64, c_int64, c_int32, c_int64, c_int32, c_double, c_int32,
                                     c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),

@@ -1,0 +1,132 @@
+"""Integer-exact wave-per-stream kernels (csrc/aa_exact.hip) for int16 I/Q input.
+
+For int16 samples every product and window sum is an exact integer, so the exact kernels and
+the general LDS engine (forced with OFS_EXACT=0) must agree BIT FOR BIT although they sum in
+different orders: P, R, M, valid and the events of sync_aa (sync_aa.py:421-571); all eight
+arrays and the gate events of minn_rtl (minn_rtl.py:583-825).  Integer arrays are also checked
+against the CPU oracle (bit-exact), which is itself pinned to the reference's goldens.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from ofdm_sync_amd import _lib, minn_rtl, sync_aa  # noqa: E402
+
+RTL_KEYS = ("corr_total", "corr_positive", "smooth_metric", "energy_total", "corr_scaled",
+            "energy_scaled", "metric_valid", "above_threshold")
+
+
+def _int12_bursts(rng, B, nb, T, blocks, amp=1500, noise=60):
+    """int16 I/Q [B, nb, T, 2]: int12 noise plus, in every other stream, a burst made of the
+    given block pattern (e.g. [1, 1] for [A][A], [1, 1, -1, -1] for Minn) of a random segment."""
+    x = rng.normal(0, noise, (B, nb, T)) + 1j * rng.normal(0, noise, (B, nb, T))
+    seg = len(blocks[1])
+    for b in range(0, B, 2):
+        n = seg * len(blocks[0])
+        if T > n + 2:
+            s = int(rng.integers(0, T - n))
+            a = rng.normal(0, amp / 3, seg) + 1j * rng.normal(0, amp / 3, seg)
+            burst = np.concatenate([sgn * a for sgn in blocks[0]])
+            x[b, :, s:s + n] += burst
+    re = np.clip(np.round(x.real), -2048, 2047)
+    im = np.clip(np.round(x.imag), -2048, 2047)
+    return np.stack([re, im], axis=-1).astype(np.int16)
+
+
+def _aa_run(xt, L, monkeypatch, exact: bool):
+    monkeypatch.setenv("OFS_EXACT", "1" if exact else "0")
+    out = sync_aa.aa_detect_streaming_batched(xt, L=L, threshold=0.15, hysteresis=16)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("B,nb,T,L", [(37, 1, 1024, 128), (9, 2, 999, 256), (5, 1, 5000, 512),
+                                      (6, 2, 700, 64), (3, 1, 2300, 1024)])
+def test_aa_exact_kernel_bit_identical_to_general_engine(B, nb, T, L, monkeypatch):
+    rng = np.random.default_rng(B * 7 + L)
+    iq = _int12_bursts(rng, B, nb, T, ([1, 1], np.zeros(L)))
+    xt = torch.from_numpy(iq).cuda()
+    plan = _lib.lib().ofs_aa_plan(_lib.CI16, _lib.FP64, nb, T, L)
+    assert 2000 < plan < 3000, plan                    # the exact kernel serves this shape
+    a = _aa_run(xt, L, monkeypatch, True)
+    g = _aa_run(xt, L, monkeypatch, False)
+    for k in ("P", "R", "M", "valid", "n_events"):
+        assert torch.equal(getattr(a, k), getattr(g, k)), k
+    n = a.n_events.cpu().numpy()
+    assert n[::2].sum() > 0                            # bursts open gates
+    for b in range(B):
+        assert torch.equal(a.ev_int[b, :n[b]], g.ev_int[b, :n[b]])
+        assert torch.equal(a.ev_real[b, :n[b]], g.ev_real[b, :n[b]])
+    for b in (0, B - 1):                               # and the oracle (integer P, R exact)
+        xc = (iq[b, ..., 0] + 1j * iq[b, ..., 1]).astype(np.complex128)
+        P, R, M, v = O.aa_metric(xc, L)
+        assert np.array_equal(a.P[b].cpu().numpy(), P)
+        assert np.array_equal(a.R[b].cpu().numpy(), R)
+        assert np.max(np.abs(a.M[b].cpu().numpy() - M)) < 1e-12
+        assert np.array_equal(a.valid[b].cpu().numpy(), v)
+
+
+def _rtl_run(xt, Q, monkeypatch, exact, **kw):
+    monkeypatch.setenv("OFS_EXACT", "1" if exact else "0")
+    out = minn_rtl.minn_rtl_batched(xt, Q, **kw)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("B,nb,T,Q", [(33, 1, 1024, 64), (7, 2, 777, 64), (5, 3, 3000, 128),
+                                      (4, 1, 4096, 512), (6, 2, 2500, 256)])
+@pytest.mark.parametrize("mode,shift,hyst", [("float", 3, 2), ("floor", 3, 2), ("float", 0, 0)])
+def test_rtl_exact_kernel_bit_identical_to_general_engine(B, nb, T, Q, mode, shift, hyst, monkeypatch):
+    rng = np.random.default_rng(B + Q + shift)
+    iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q)))
+    xt = torch.from_numpy(iq).cuda()
+    assert _lib.lib().ofs_rtl_plan(_lib.CI16, nb, T, Q) > 2000
+    kw = dict(smooth_shift=shift, threshold_value=3276, threshold_frac_bits=15, smooth_mode=mode,
+              hysteresis=hyst, timing_offset=-5)
+    a = _rtl_run(xt, Q, monkeypatch, True, **kw)
+    g = _rtl_run(xt, Q, monkeypatch, False, **kw)
+    for k in RTL_KEYS + ("n_events", "open_gate_start"):
+        assert torch.equal(getattr(a, k), getattr(g, k)), k
+    n = a.n_events.cpu().numpy()
+    assert n.sum() > 0
+    for b in range(B):
+        m = min(int(n[b]), a.events.shape[1])
+        assert torch.equal(a.events[b, :m], g.events[b, :m])
+    xc = (iq[0, ..., 0] + 1j * iq[0, ..., 1]).astype(np.complex128)
+    s = O.minn_rtl_metric(xc, Q, shift, 3276, 15, smooth_mode=mode)
+    for k in RTL_KEYS:
+        assert np.array_equal(getattr(a, k)[0].cpu().numpy(), s[k]), k
+    ev, _, _ = O.detect_minn_rtl(s["corr_positive"], s["above_threshold"], s["metric_valid"], hyst, -5)
+    assert np.array_equal(a.events[0, :int(n[0])].cpu().numpy(), ev)
+
+
+def test_rtl_exact_metric_only_outputs(monkeypatch):
+    """Metric without smoothing outputs or gate (the optional arrays of ofs_minn_rtl are null
+    except corr_total / energy_total): exact kernel skips the sequential pass."""
+    rng = np.random.default_rng(3)
+    iq = _int12_bursts(rng, 4, 1, 1024, ([1, 1, -1, -1], np.zeros(64)))
+    xt = torch.from_numpy(iq).cuda()
+    B, T = 4, 1024
+    ct = torch.empty((B, T), dtype=torch.float64, device="cuda")
+    et = torch.empty_like(ct)
+    rc = _lib.lib().ofs_minn_rtl(_lib.CI16, xt.data_ptr(), B, 1, T, 64, 3, 0, 3276, 15, ct.data_ptr(),
+                                 None, None, et.data_ptr(), None, None, None, None, 0, 0, 0, 0, None,
+                                 None, None, _lib.stream_ptr())
+    assert rc == 0
+    ref = minn_rtl.minn_rtl_batched(xt, 64, detect=False)
+    assert torch.equal(ct, ref.corr_total) and torch.equal(et, ref.energy_total)
+
+
+def test_exact_plans_fall_back_outside_exact_range():
+    L_ = _lib.lib()
+    assert L_.ofs_aa_plan(_lib.CI16, _lib.FP64, 1, 1024, 192) < 2000          # L not covered
+    assert L_.ofs_aa_plan(_lib.C128, _lib.FP64, 1, 1024, 128) < 2000          # float input
+    assert L_.ofs_aa_plan(_lib.CI16, _lib.FP64, 1, (1 << 21) + 2, 128) < 2000  # sums may pass 2^53
+    assert L_.ofs_rtl_plan(_lib.CI16, 1, 1024, 1024) == 0                     # Q > 512
+    assert L_.ofs_rtl_plan(_lib.C128, 1, 1024, 64) == 0

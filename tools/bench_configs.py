@@ -70,8 +70,11 @@ def cfg2a(dev, st, steps, warmup):
             st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa"), steps, warmup, st)
     nbytes = B * T * (4 + 16 + 8 + 8 + 1)
+    plan = L_.ofs_aa_plan(_lib.CI16, _lib.FP64, 1, T, L)
+    kernel = (f"aa_exact_kernel<E={(plan - 2000) // 10},MR={plan % 10}> (integer-exact, wave per stream, "
+              "fused events)" if plan > 2000 else "win_kernel<CI16,fp64,AA> (fused events)")
     return dict(config="cfg2a", workload=f"sync_aa detector L={L}, int12 I/Q, {B} x {T}, fp64",
-                kernel="win_kernel<CI16,fp64,AA> (fused events)", samples=B * T, ms=ms, alg_bytes=nbytes,
+                kernel=kernel, samples=B * T, ms=ms, alg_bytes=nbytes,
                 bytes_per_sample="4 in + P 16 + R 8 + M 8 + valid 1")
 
 
@@ -91,8 +94,11 @@ def cfg2b(dev, st, steps, warmup):
             n_ev.data_ptr(), ev.data_ptr(), og.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_minn_rtl(*args), "minn_rtl"), steps, warmup, st)
     nbytes = B * T * (4 + 6 * 8 + 2)
+    plan = L_.ofs_rtl_plan(_lib.CI16, 1, T, Q)
+    kernel = (f"rtl_exact_kernel<E={(plan - 2000) // 10},MW={plan % 10}> (integer-exact metric + in-wave "
+              "IIR + closed-form gate)" if plan else "win_kernel<CI16,fp64,RTL> + rtl_iir_kernel")
     return dict(config="cfg2b", workload=f"minn_rtl Q={Q}, int12 I/Q, {B} x {T}, fp64 + sequential IIR/gate",
-                kernel="win_kernel<CI16,fp64,RTL> + rtl_iir_kernel", samples=B * T, ms=ms, alg_bytes=nbytes,
+                kernel=kernel, samples=B * T, ms=ms, alg_bytes=nbytes,
                 bytes_per_sample="4 in + 6 x f64 8 + 2 flags")
 
 
