@@ -234,6 +234,46 @@ int32_t ofs_zc_gate(const double* corr_mag, const uint8_t* above_threshold, cons
                     uint8_t* gate_mask, int32_t max_events, int32_t* n_events, int64_t* ev_int,
                     double* ev_peak, void* stream);
 
+/* ---- detection post-processing (metric streams -> timing decisions) -------------------------
+ * Metrics are [B][n] device arrays; `precision` names their element type (OFS_FP32 = float,
+ * OFS_FP64 = double).  Smoothed outputs are f64.  Per-stream `status` reports what the
+ * reference would do: >= 0 ok (for ofs_plateau_end the branch taken), < 0 it raises ValueError.
+ */
+
+/* minn._trailing_average / combined_sc_min._trailing_average (minn.py:115-128,
+ * combined_sc_min.py:167-180) of max(x, 0) when clip_negative != 0 (minn.py:149), else of x:
+ * the reference's float64 running-sum recursion, sample by sample.  out: [B][n] f64. */
+int32_t ofs_trailing_average(int32_t precision, const void* x, int64_t B, int64_t n, int32_t win,
+                             int32_t clip_negative, double* out, void* stream);
+
+/* sc.find_plateau_end_from_metric (sc.py:81-146).  lookahead < 0 means None.  Ms: [B][max(n, w)]
+ * f64 (numpy "same" convolution length); plateau_end: [B] int64; status: [B] int32 = branch
+ * (1 drop below 95 %, 2 earliest long run above 60 %, 3 slope fallback, 4 fallback on an empty
+ * window, 0 empty metric), -3 where numpy's broadcast would raise. */
+int32_t ofs_plateau_end(int32_t precision, const void* M, int64_t B, int64_t n, int32_t cp_len,
+                        int32_t lookahead, int32_t smooth_win, double* Ms, int64_t* plateau_end,
+                        int32_t* status, void* stream);
+
+/* minn.find_minn_peak (minn.py:131-205) on the trailing average Ms (ofs_trailing_average):
+ * gate = longest run of Ms >= gate_threshold * max(Ms) (earliest on ties) cut to
+ * [bound_lo, bound_hi) (0, n for no bounds); empty gate -> global argmax.  peak, gate_lo,
+ * gate_hi: [B] int64 (gate_* nullable); status -1 empty metric, -2 no positive peak. */
+int32_t ofs_minn_peak(const double* Ms, int64_t B, int64_t n, double gate_threshold, int64_t bound_lo,
+                      int64_t bound_hi, int64_t* peak, int64_t* gate_lo, int64_t* gate_hi, int32_t* status,
+                      void* stream);
+
+/* The S&C gate of combined_sc_min.run_simulation (combined_sc_min.py:337-358):
+ * mask = M_sc / max >= threshold (max > 0) else M_sc >= threshold, seeded with the argmax when
+ * empty.  mask: [B][n] uint8 (nullable); span: [B][2] int64 = first, last + 1 (nullable). */
+int32_t ofs_sc_gate(int32_t precision, const void* M_sc, int64_t B, int64_t n, double threshold,
+                    uint8_t* mask, int64_t* span, void* stream);
+
+/* combined_sc_min._streaming_peak_detector (combined_sc_min.py:183-209) as used by
+ * combined_sc_min.find_minn_peak (:212-259): first argmax (strict >) of Ms over the FIRST run of
+ * mask within [bound_lo, bound_hi).  peak: [B] int64; status -1 empty gate region. */
+int32_t ofs_segment_peak(const double* Ms, const uint8_t* mask, int64_t B, int64_t n, int64_t bound_lo,
+                         int64_t bound_hi, int64_t* peak, int32_t* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

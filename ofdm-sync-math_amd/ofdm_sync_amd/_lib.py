@@ -52,6 +52,12 @@ def _declare(lib):
                                          P, P, P, P, P]),
         "ofs_win_plan": (c_int32, [c_int32, c_int32, c_int32, c_int32, c_int64, c_int32]),
         "ofs_rtl_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32]),
+        "ofs_trailing_average": (c_int32, [c_int32, P, c_int64, c_int64, c_int32, c_int32, P, P]),
+        "ofs_plateau_end": (c_int32, [c_int32, P, c_int64, c_int64, c_int32, c_int32, c_int32, P, P, P,
+                                      P]),
+        "ofs_minn_peak": (c_int32, [P, c_int64, c_int64, c_double, c_int64, c_int64, P, P, P, P, P]),
+        "ofs_sc_gate": (c_int32, [c_int32, P, c_int64, c_int64, c_double, P, P, P]),
+        "ofs_segment_peak": (c_int32, [P, P, c_int64, c_int64, c_int64, c_int64, P, P, P]),
         "ofs_zc_freq_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32, c_int32]),
         "ofs_zc_detect": (c_int32, [P, c_int64, c_int64, c_int32, c_int64, c_int32, c_double, c_int32,
                                     c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),

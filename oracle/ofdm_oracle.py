@@ -26,6 +26,7 @@ __all__ = [
     "minn_rtl_metric", "detect_minn_rtl", "cp_cfo",
     "park_metric", "zc_template", "zc_freq_metric", "pss_symbol", "matched_filter",
     "normalize_correlation", "zc_combined", "zc_streaming_detection", "detect_zc_peaks",
+    "trailing_average", "plateau_end", "minn_peak", "sc_gate", "streaming_peak", "comb_minn_peak",
 ]
 
 
@@ -481,3 +482,155 @@ def detect_zc_peaks(corr_mag, above, valid, reference_length, hysteresis):
         vals.append(peak_value)
         mask[gate_start:n] = True
     return np.array(evs, np.int64).reshape(-1, 4), np.array(vals, np.float64), mask
+
+
+# ---------------------------------------------------------------------------------------
+# Detection post-processing: turns a metric stream into a timing decision.
+# ---------------------------------------------------------------------------------------
+def trailing_average(x, win):
+    """minn._trailing_average (minn.py:115-128) == combined_sc_min._trailing_average
+    (combined_sc_min.py:167-180): the running sum adds x[i] and drops x[i-win], divided by the
+    number of samples seen (capped at win).  Literal float64 recursion."""
+    x = np.asarray(x, dtype=float)
+    if win <= 1:
+        return x.copy()
+    y = np.empty_like(x)
+    acc = 0.0
+    for i in range(x.size):
+        acc += x[i]
+        if i >= win:
+            acc -= x[i - win]
+        y[i] = acc / (win if i >= win - 1 else i + 1)
+    return y
+
+
+def _runs(mask):
+    """[start, end) of the True runs of a boolean mask, in order."""
+    m = np.concatenate(([False], np.asarray(mask, bool), [False]))
+    d = np.flatnonzero(m[1:] != m[:-1])
+    return list(zip(d[0::2], d[1::2]))
+
+
+def _py_slice(n, start, stop):
+    """Indices of a[start:stop] for len(a) == n (Python slice semantics, step 1)."""
+    return range(n)[start:stop]
+
+
+def plateau_end(M, cp_len, lookahead=None, smooth_win=8):
+    """sc.find_plateau_end_from_metric (sc.py:81-146).  Returns (index, branch, Ms) with branch
+    1 = first drop below 95 % of the smoothed maximum (:106-114), 2 = right edge of the earliest
+    run >= max(8, cp/2) above 60 % (:117-133), 3 = slope fallback (:136-146), 4 = fallback with
+    an empty drop window (:142-143), 0 = empty metric."""
+    M = np.asarray(M, dtype=float)
+    if M.size == 0:
+        return 0, 0, M.copy()
+    L = (cp_len // 4) if lookahead is None else int(max(1, lookahead))
+    w = max(1, smooth_win)
+    Ms = np.convolve(M, np.ones(w, dtype=float) / w, mode="same")
+    center = int(np.argmax(Ms))
+    post_hi = min(Ms.size, center + cp_len)
+    if post_hi > center + 1:
+        below = np.flatnonzero(Ms[center:post_hi] <= 0.95 * float(Ms[center]))
+        if below.size > 0:
+            return int(center + below[0]), 1, Ms
+    min_run = max(8, cp_len // 2)
+    peak = float(np.max(Ms))
+    if peak > 0:
+        for s, e in _runs(Ms >= 0.6 * peak):
+            if e - s >= min_run:
+                return int(e - 1), 2, Ms
+    lo = max(0, center - cp_len)
+    hi = min(Ms.size - L - 1, center + cp_len)
+    win_idx = _py_slice(Ms.size, lo, hi)
+    ahead_idx = _py_slice(Ms.size, lo + L, hi + L)
+    window, ahead = Ms[list(win_idx)], Ms[list(ahead_idx)]
+    drop = window - ahead              # numpy broadcasting rules (raises on a length mismatch)
+    if drop.size == 0:
+        return center, 4, Ms
+    return lo + int(np.argmax(drop)) + (L // 2), 3, Ms
+
+
+def _bounds(n, search_bounds):
+    if search_bounds is None:
+        return 0, n
+    start, end = max(0, search_bounds[0]), min(n, search_bounds[1])
+    return (0, n) if start >= end else (start, end)
+
+
+def minn_peak(M, smooth_win=8, gate_threshold=0.5, search_bounds=None):
+    """minn.find_minn_peak (minn.py:131-205): (peak_idx, gate_mask, Ms).  The gate is the
+    LONGEST run of Ms >= gate_threshold * max(Ms) (earliest on ties), cut to the search bounds;
+    an empty gate falls back to the global argmax.  Raises ValueError like the reference."""
+    M = np.asarray(M, dtype=float)
+    if M.size == 0:
+        raise ValueError("Minn metric is empty")
+    Ms = trailing_average(np.maximum(M, 0.0), max(1, smooth_win))
+    mx = float(np.max(Ms))
+    if mx <= 0.0:
+        raise ValueError("Minn metric did not produce a positive peak")
+    gate = np.zeros(M.size, bool)
+    best = None
+    for s, e in _runs(Ms >= gate_threshold * mx):
+        if best is None or e - s > best[1] - best[0]:
+            best = (s, e)
+    if best is not None:
+        gate[best[0]:best[1]] = True
+    lo, hi = _bounds(M.size, search_bounds)
+    if search_bounds is not None:
+        b = np.zeros(M.size, bool)
+        b[lo:hi] = True
+        gate &= b
+    if not gate.any():
+        pk = int(np.argmax(Ms))
+        gate = np.zeros(M.size, bool)
+        gate[pk] = True
+        return pk, gate, Ms
+    idx = np.flatnonzero(gate)
+    return int(idx[int(np.argmax(Ms[idx]))]), gate, Ms
+
+
+def sc_gate(M_sc, threshold=0.6):
+    """The S&C gate of combined_sc_min.run_simulation (combined_sc_min.py:337-358): normalise by
+    the maximum, threshold, seed with the argmax if nothing passes.  Returns (mask, span)."""
+    M_sc = np.asarray(M_sc, dtype=float)
+    mx = float(np.max(M_sc))
+    mask = (M_sc / mx >= threshold) if mx > 0 else (M_sc >= threshold)
+    if not mask.any():
+        mask = np.zeros(M_sc.size, bool)
+        mask[int(np.argmax(M_sc))] = True
+    idx = np.flatnonzero(mask)
+    return mask, (int(idx[0]), int(idx[-1]) + 1)
+
+
+def streaming_peak(metric, gate_mask):
+    """combined_sc_min._streaming_peak_detector (combined_sc_min.py:183-209): first argmax
+    (strict >) over the FIRST run of the gate; None if the gate never opens."""
+    best_idx, best_val, active = None, -np.inf, False
+    for i, v in enumerate(metric):
+        if gate_mask[i]:
+            if not active:
+                active, best_val, best_idx = True, v, i
+            elif v > best_val:
+                best_val, best_idx = v, i
+        elif active:
+            return best_idx
+    return best_idx
+
+
+def comb_minn_peak(M, smooth_win, gate_mask, search_bounds=None):
+    """combined_sc_min.find_minn_peak (combined_sc_min.py:212-259)."""
+    M = np.asarray(M, dtype=float)
+    if M.size == 0:
+        return 0
+    mask = np.asarray(gate_mask, bool).copy()
+    if mask.shape[0] != M.shape[0]:
+        raise ValueError("gate_mask must match metric length")
+    if search_bounds is not None:
+        lo, hi = _bounds(M.size, search_bounds)
+        b = np.zeros(M.size, bool)
+        b[lo:hi] = True
+        mask &= b
+    if not mask.any():
+        raise ValueError("Minn peak detector received empty gate region")
+    Ms = trailing_average(np.maximum(M, 0.0), max(1, smooth_win))
+    return streaming_peak(Ms, mask)

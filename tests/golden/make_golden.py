@@ -321,6 +321,86 @@ def gen_zc(R, cases):
                           min_corr_mag=np.float64(z2.MIN_CORR_MAG), hysteresis=np.int64(z2.HYSTERESIS))
 
 
+def gen_post(R, cases):
+    """Detection post-processing on metrics the reference produced above:
+    sc.find_plateau_end_from_metric (sc.py:81-146), minn.find_minn_peak (minn.py:131-205),
+    minn._trailing_average (minn.py:115-128), combined_sc_min.find_minn_peak (:212-259) with
+    _streaming_peak_detector (:183-209), and the S&C gate of combined_sc_min.run_simulation
+    (:337-358, inline code restated here statement for statement)."""
+    sc, minn, comb = R["sc"], R["minn"], R["combined"]
+    rng = np.random.default_rng(11)
+    # ---- sc plateau end: reference metrics + shapes that reach the other branches ----
+    pl = []
+    for name, cp, la, sw in (("sc_N2048_cir1", 512, 128, 16), ("sc_N1024_cir2_2br", 256, 64, 16),
+                             ("sc_N64_cfg1", 16, None, 8), ("sc_N2048_cir1", 512, None, 8)):
+        pl.append((cases[name]["M"], cp, la, sw))
+    ramp = np.linspace(0.0, 1.0, 300)
+    spikes = np.zeros(400)
+    spikes[::37] = rng.uniform(0.2, 1.0, spikes[::37].size)
+    plateau = np.concatenate([np.full(50, 0.1), np.full(120, 0.9), np.full(80, 0.2)])
+    pl += [(ramp, 64, None, 8), (spikes, 1, None, 1), (spikes, 3, 2, 4), (np.zeros(100), 16, None, 8),
+           (plateau, 40, None, 1), (plateau[::-1].copy(), 1, 5, 1), (rng.random(257), 2, 1, 3),
+           (np.array([0.3]), 16, None, 8), (np.array([0.1, 0.5]), 1, None, 1), (np.zeros(0), 16, None, 8)]
+    for i, (M, cp, la, sw) in enumerate(pl):
+        try:
+            out = np.int64(sc.find_plateau_end_from_metric(np.asarray(M, float), cp, lookahead=la, smooth_win=sw))
+            err = np.int64(0)
+        except ValueError:
+            out, err = np.int64(-1), np.int64(1)
+        cases[f"post_plateau_{i:02d}"] = dict(kind="plateau", M=np.asarray(M, float), cp=np.int64(cp),
+                                              lookahead=np.int64(-1 if la is None else la),
+                                              smooth_win=np.int64(sw), index=out, error=err)
+    # ---- minn.find_minn_peak ----
+    mp = [(cases["comb_minn_N2048_cir1_2br"]["M"], 16, 0.5, None),
+          (cases["minn_param_N256"]["M"], 8, 0.5, None),
+          (cases["minn_param_N512"]["M"], 16, 0.5, (100, 900)),
+          (cases["minn_param_N512"]["M"], 1, 0.7, (2000, 1000)),        # start >= end: whole range
+          (cases["comb_minn_N2048_cir1_2br"]["M"], 16, 0.5, (0, 50)),    # bounds miss the gate
+          (np.concatenate([rng.random(40) * 0.1, [0.9] * 5, [0.1] * 10, [0.8] * 5, rng.random(30) * 0.1]),
+           1, 0.5, None),                                              # two equal runs: earliest wins
+          (-np.abs(rng.standard_normal(64)), 4, 0.5, None),              # no positive peak: ValueError
+          (np.zeros(0), 4, 0.5, None)]                                   # empty: ValueError
+    for i, (M, sw, thr, bnd) in enumerate(mp):
+        M = np.asarray(M, float)
+        try:
+            pk, gate, Ms = minn.find_minn_peak(M, smooth_win=sw, gate_threshold=thr, search_bounds=bnd)
+            err = np.int64(0)
+        except ValueError:
+            pk, gate, Ms, err = -1, np.zeros(M.size, bool), np.zeros(M.size), np.int64(1)
+        cases[f"post_minnpeak_{i:02d}"] = dict(
+            kind="minn_peak", M=M, smooth_win=np.int64(sw), thr=np.float64(thr),
+            bounds=np.array([-1, -1] if bnd is None else bnd, np.int64), peak=np.int64(pk),
+            gate=np.asarray(gate, bool), Ms=np.asarray(Ms, float), error=err)
+    cases["post_trailing_avg"] = dict(
+        kind="trailing", x=np.maximum(cases["comb_minn_N2048_cir1_2br"]["M"], 0.0),
+        y16=comb._trailing_average(np.maximum(cases["comb_minn_N2048_cir1_2br"]["M"], 0.0), win=16),
+        y1=minn._trailing_average(np.maximum(cases["comb_minn_N2048_cir1_2br"]["M"], 0.0), win=1),
+        y3=minn._trailing_average(np.maximum(cases["minn_param_N256"]["M"], 0.0), win=3),
+        x3=np.maximum(cases["minn_param_N256"]["M"], 0.0))
+    # ---- combined_sc_min back end: S&C gate -> find_minn_peak on the Minn metric ----
+    M_sc, M_mn = cases["comb_sc_N2048_cir1_2br"]["M"], cases["comb_minn_N2048_cir1_2br"]["M"]
+    max_sc = float(np.max(M_sc))                                        # combined_sc_min.py:340-355
+    gate = (M_sc / max_sc >= comb.SC_GATE_THRESHOLD) if max_sc > 0 else (M_sc >= comb.SC_GATE_THRESHOLD)
+    if not np.any(gate):
+        gate = np.zeros_like(gate, dtype=bool)
+        gate[int(np.argmax(M_sc))] = True
+    first, last = int(np.argmax(gate)), int(gate.size - np.argmax(gate[::-1]) - 1)
+    pk = comb.find_minn_peak(M_mn, smooth_win=comb.SMOOTH_WIN, gate_mask=gate, search_bounds=None)
+    cases["post_comb_detect"] = dict(kind="comb_detect", M_sc=M_sc, M_minn=M_mn, gate=gate,
+                                     span=np.array([first, last + 1], np.int64), peak=np.int64(pk),
+                                     smooth_win=np.int64(comb.SMOOTH_WIN))
+    # streaming peak on multi-run masks (first run only), metrics with ties
+    met = np.round(rng.random(500) * 8) / 8
+    sp = {}
+    for j in range(4):
+        mask = rng.random(500) < (0.02, 0.2, 0.6, 0.0)[j]
+        sp[f"mask{j}"] = mask
+        r = comb._streaming_peak_detector(met, mask)
+        sp[f"peak{j}"] = np.int64(-1 if r is None else r)
+    pk_b = comb.find_minn_peak(M_mn, smooth_win=4, gate_mask=gate, search_bounds=(first + 5, last - 5))
+    cases["post_streaming_peak"] = dict(kind="streaming_peak", metric=met, peak_bounded=np.int64(pk_b), **sp)
+
+
 def main():
     R = _import_reference()
     cases: dict[str, dict] = {}
@@ -331,6 +411,7 @@ def main():
     gen_cp_cfo(R, cases)
     gen_park(R, cases)
     gen_zc(R, cases)
+    gen_post(R, cases)
     OUT.mkdir(parents=True, exist_ok=True)
     for name, d in cases.items():
         arrs = {k: (np.asarray(v) if not isinstance(v, str) else np.array(v)) for k, v in d.items()}

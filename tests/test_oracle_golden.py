@@ -103,6 +103,35 @@ def test_oracle_matches_reference_golden(path):
                                            N, int(d["hysteresis"]))
         assert np.array_equal(ev, d["events"]) and np.array_equal(vals, d["peak_values"])
         assert np.array_equal(mask, d["gate_mask"])
+    elif kind == "plateau":
+        la = None if int(d["lookahead"]) < 0 else int(d["lookahead"])
+        if int(d["error"]):
+            with pytest.raises(ValueError):
+                O.plateau_end(d["M"], int(d["cp"]), la, int(d["smooth_win"]))
+        else:
+            idx, _, _ = O.plateau_end(d["M"], int(d["cp"]), la, int(d["smooth_win"]))
+            assert idx == int(d["index"])
+    elif kind == "minn_peak":
+        b = None if int(d["bounds"][0]) < 0 else (int(d["bounds"][0]), int(d["bounds"][1]))
+        if int(d["error"]):
+            with pytest.raises(ValueError):
+                O.minn_peak(d["M"], int(d["smooth_win"]), float(d["thr"]), b)
+        else:
+            pk, gate, Ms = O.minn_peak(d["M"], int(d["smooth_win"]), float(d["thr"]), b)
+            assert pk == int(d["peak"])
+            assert np.array_equal(gate, d["gate"]) and np.array_equal(Ms, d["Ms"])   # literal recursion
+    elif kind == "trailing":
+        assert np.array_equal(O.trailing_average(d["x"], 16), d["y16"])
+        assert np.array_equal(O.trailing_average(d["x"], 1), d["y1"])
+        assert np.array_equal(O.trailing_average(d["x3"], 3), d["y3"])
+    elif kind == "comb_detect":
+        mask, span = O.sc_gate(d["M_sc"])
+        assert np.array_equal(mask, d["gate"]) and span == tuple(int(v) for v in d["span"])
+        assert O.comb_minn_peak(d["M_minn"], int(d["smooth_win"]), mask) == int(d["peak"])
+    elif kind == "streaming_peak":
+        for j in range(4):
+            r = O.streaming_peak(d["metric"], d[f"mask{j}"])
+            assert (-1 if r is None else r) == int(d[f"peak{j}"])
     else:
         pytest.fail(kind)
 
