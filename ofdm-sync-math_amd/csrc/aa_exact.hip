@@ -212,23 +212,26 @@ template <int E, int MODE>
 __device__ __forceinline__ void smooth_row(const double (&c)[E], double (&out)[E], double& sm, long long& si,
                                            int lane, int cnt, int vfrom, double inv, int shift) {
 #pragma clang fp contract(off)
-    const int lanes = (cnt + E - 1) / E;
-    for (int l = 0; l < lanes; ++l) {
+    const int jf = vfrom < cnt ? vfrom : cnt;                     // positions before jf: state holds
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (E * lane + e < jf) out[e] = sm;
+    const int l1 = (cnt + E - 1) / E;
+#pragma unroll 2
+    for (int l = jf / E; l < l1; ++l) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int j = E * l + e;
-            if (j < cnt) {
-                if (j >= vfrom) {
-                    const double cj = readlane(c[e], l);
-                    if constexpr (MODE == 0) {
-                        sm = sm + (cj - sm) * inv;
-                    } else if constexpr (MODE == 1) {
-                        sm = cj;
-                    } else {
-                        const long long ci = (long long)cj;
-                        si = (shift == 0) ? ci : si + ((ci - si) >> shift);
-                        sm = (double)si;
-                    }
+            if (j >= jf && j < cnt) {
+                const double cj = readlane(c[e], l);
+                if constexpr (MODE == 0) {
+                    sm = sm + (cj - sm) * inv;
+                } else if constexpr (MODE == 1) {
+                    sm = cj;
+                } else {
+                    const long long ci = (long long)cj;
+                    si = (shift == 0) ? ci : si + ((ci - si) >> shift);
+                    sm = (double)si;
                 }
                 if (lane == l) out[e] = sm;
             }
@@ -297,22 +300,53 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
         gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
                   nullptr, a.toff);
 
+    // rows stream in PD rows ahead of use (register queue shifted by one row per step)
+    constexpr int PD = E == 1 ? 8 : (E == 2 ? 4 : 2);
+    constexpr int NBM = 4;                                         // branches supported
+    int32_t nx[PD][NBM][E];
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+#pragma unroll
+        for (int t = 0; t < NBM; ++t) {
+            if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
+            else
+#pragma unroll
+                for (int e = 0; e < E; ++e) nx[p][t][e] = 0;
+        }
+
     for (int k = 0; k < nrows; ++k) {
         const int nb = RL * k + E * lane;
         const int xsl = k % MW;
+        int32_t cur[NBM][E];
+#pragma unroll
+        for (int t = 0; t < NBM; ++t)
+#pragma unroll
+            for (int e = 0; e < E; ++e) cur[t][e] = nx[0][t][e];
+#pragma unroll
+        for (int p = 0; p + 1 < PD; ++p)
+#pragma unroll
+            for (int t = 0; t < NBM; ++t)
+#pragma unroll
+                for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
+        if (k + PD < nrows) {
+#pragma unroll
+            for (int t = 0; t < NBM; ++t)
+                if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[PD - 1][t]);
+        }
         double pc[E], en[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
-        for (int t = 0; t < nb_; ++t) {
-            int32_t cur[E];
-            load_words<E>(xs + t * T, nb, T, cur);
 #pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int32_t d = hx(t, xsl, e);
-                const double xr = w_re(cur[e]), xi = w_im(cur[e]);
-                pc[e] += w_re(d) * xr + w_im(d) * xi;                // minn_rtl.py:616, exact
-                en[e] += xr * xr + xi * xi;                           // :617
-                hx(t, xsl, e) = cur[e];
+        for (int t = 0; t < NBM; ++t) {
+            if (t < nb_) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int32_t d = hx(t, xsl, e);
+                    const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
+                    pc[e] += w_re(d) * xr + w_im(d) * xi;            // minn_rtl.py:616, exact
+                    en[e] += xr * xr + xi * xi;                       // :617
+                    hx(t, xsl, e) = cur[t][e];
+                }
             }
         }
         RowPrefix<E> qc, qe;

@@ -90,7 +90,12 @@ def cfg2b(dev, st, steps, warmup):
     ev = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
     og = torch.empty(B, dtype=torch.int64, device=dev)
     L_ = _lib.lib()
-    args = (_lib.CI16, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *[t.data_ptr() for t in o], 1, 2, 0, E,
+    parts = os.environ.get("OFS_CFG2B_PARTS", "full")       # diagnostic: metric | smooth | full
+    ptrs = [t.data_ptr() for t in o]
+    if parts == "metric":
+        ptrs = [ptrs[0], ptrs[1], None, ptrs[3], None, ptrs[5], ptrs[6], None]
+    det = 0 if parts in ("metric", "smooth") else 1
+    args = (_lib.CI16, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *ptrs, det, 2, 0, E,
             n_ev.data_ptr(), ev.data_ptr(), og.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_minn_rtl(*args), "minn_rtl"), steps, warmup, st)
     nbytes = B * T * (4 + 6 * 8 + 2)
