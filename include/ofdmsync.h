@@ -170,6 +170,27 @@ int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64
                    double* P_out, double* cfo_out, void* stream);
 
 /*
+ * CP-correlation searches around an estimated CP start est[b], with
+ * P_w(d) = sum_br sum_{n<win_len} x[d+n]·conj(x[d+n+n_fft]) over d in
+ * [max(0, est - span), min(T - (n_fft + win_len), est + span)):
+ *   mode OFS_CPS_ROBUST (0): cfo from the angle of sum_d P_w(d) — replaces
+ *        core.estimate_cfo_from_cp_robust (core.py:199-231) with win_len = its `win`;
+ *   mode OFS_CPS_PEAK (1):   d* = first argmax |P_w(d)|, cfo from P_w(d*) — replaces
+ *        core.estimate_cfo_from_cp_peak / _peak_with_index (core.py:234-303) and
+ *        core.find_cp_start_via_corr (core.py:306-336; span = search_half) with win_len = cp_len.
+ * est: [B] int64; P_out [B][2] f64 and d_out [B] int64 nullable; cfo_out [B] f64;
+ * status [B] int32: 0 searched, 1 empty range (the reference then falls back to
+ * estimate_cfo_from_cp at est: the caller runs ofs_cp_cfo; d_out = est, cfo_out = NaN).
+ * Windows are summed directly in fp64 (no prefix differences).
+ */
+#define OFS_CPS_ROBUST 0
+#define OFS_CPS_PEAK   1
+int32_t ofs_cp_search(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                      const int64_t* est, int32_t n_fft, int32_t win_len, int32_t span,
+                      int32_t mode, double fs_hz, double* P_out, int64_t* d_out,
+                      double* cfo_out, int32_t* status, void* stream);
+
+/*
  * Park mirror-symmetry metric: replaces park.park_streaming_metric (park.py:64-114).
  * half = N/2; outputs for d in [half, T-half-1], n_out = T - 2*half, laid out [B][n_out]:
  *   P (c64|c128) = sum_br sum_{k<half} x[d-k]*x[d+k]; E (f32|f64) = sum_br sum_{k<half}|x[d+k]|^2;

@@ -23,7 +23,7 @@ import numpy as np
 __all__ = [
     "aa_metric", "aa_events", "aa_detect",
     "sc_metric", "comb_sc_metric", "minn_metric",
-    "minn_rtl_metric", "detect_minn_rtl", "cp_cfo",
+    "minn_rtl_metric", "detect_minn_rtl", "cp_cfo", "cp_cfo_robust", "cp_cfo_peak", "find_cp_start",
     "park_metric", "zc_template", "zc_freq_metric", "pss_symbol", "matched_filter",
     "normalize_correlation", "zc_combined", "zc_streaming_detection", "detect_zc_peaks",
     "trailing_average", "plateau_end", "minn_peak", "sc_gate", "streaming_peak", "comb_minn_peak",
@@ -304,6 +304,64 @@ def cp_cfo(rx, start, n_fft, cp_len, fs_hz):
     b = x[:, start + n_fft:start + n_fft + cp_len]
     P = np.sum(a * np.conj(b))
     return float(-np.angle(P) * fs_hz / (2 * np.pi * n_fft)), complex(P)
+
+
+# ---------------------------------------------------------------------------------------
+# CP-correlation searches (core.py:199-336)
+# ---------------------------------------------------------------------------------------
+def _cp_window(x, d, n_fft, w):
+    return np.sum(x[:, d:d + w] * np.conj(x[:, d + n_fft:d + n_fft + w]))
+
+
+def cp_cfo_robust(rx, est, n_fft, cp_len, fs_hz, span=None, win_len=None):
+    """core.estimate_cfo_from_cp_robust (core.py:199-231): angle of sum_d P_win(d) over
+    d in [max(0, est-span), min(T-(N+win), est+span)); empty range -> estimate_cfo_from_cp at
+    est with min(cp_len, win) samples (:222-223)."""
+    x = _as2d(rx)
+    T = x.shape[1]
+    span = cp_len // 2 if span is None else int(max(0, span))
+    win = cp_len // 2 if win_len is None else int(max(1, win_len))
+    lo, hi = max(0, est - span), min(T - (n_fft + win), est + span)
+    if hi <= lo:
+        return cp_cfo(x, est, n_fft, min(cp_len, win), fs_hz)[0]
+    P = 0j
+    for d in range(lo, hi):
+        P += _cp_window(x, d, n_fft, win)
+    return float(-np.angle(P) * fs_hz / (2 * np.pi * n_fft))
+
+
+def cp_cfo_peak(rx, est, n_fft, cp_len, fs_hz, span=None):
+    """core.estimate_cfo_from_cp_peak_with_index (core.py:271-303; estimate_cfo_from_cp_peak
+    :234-268 is its first element): first d maximising |P_cp(d)| (strict >) in the search
+    range, CFO from P_cp(d); empty range -> (estimate_cfo_from_cp at est, est)."""
+    x = _as2d(rx)
+    T = x.shape[1]
+    span = cp_len // 2 if span is None else int(max(0, span))
+    lo, hi = max(0, est - span), min(T - (n_fft + cp_len), est + span)
+    if hi <= lo:
+        return cp_cfo(x, est, n_fft, cp_len, fs_hz)[0], int(est)
+    best, bmag, bd = 0j, -1.0, lo
+    for d in range(lo, hi):
+        P = _cp_window(x, d, n_fft, cp_len)
+        m = float(np.abs(P))
+        if m > bmag:
+            best, bmag, bd = P, m, d
+    return float(-np.angle(best) * fs_hz / (2 * np.pi * n_fft)), int(bd)
+
+
+def find_cp_start(rx, est, n_fft, cp_len, search_half=1024):
+    """core.find_cp_start_via_corr (core.py:306-336)."""
+    x = _as2d(rx)
+    T = x.shape[1]
+    lo, hi = max(0, est - search_half), min(T - (n_fft + cp_len), est + search_half)
+    if hi <= lo:
+        return int(est)
+    bd, bv = lo, -1.0
+    for d in range(lo, hi):
+        v = float(np.abs(_cp_window(x, d, n_fft, cp_len)))
+        if v > bv:
+            bv, bd = v, d
+    return int(bd)
 
 
 # ---------------------------------------------------------------------------------------

@@ -239,6 +239,28 @@ def gen_cp_cfo(R, cases):
     cases["cp_cfo"] = dict(kind="cp_cfo", x=rx, starts=starts, n_fft=np.int64(2048),
                            cp_len=np.int64(512), fs=np.float64(core.SAMPLE_RATE_HZ), cfo=cfo,
                            cfo_1br_cp256=cfo1, fs_1br=np.float64(15.36e6))
+    # CP searches around an estimated start (core.py:199-336): estimates early / late / near the
+    # edges (empty range -> fallback), default and explicit span / win_len, 1 and 2 branches
+    est = np.array([0, 150, 200, 260, 1000, rx.shape[1] - 2048 - 512 - 3, rx.shape[1] - 2048 - 512], np.int64)
+    fs = core.SAMPLE_RATE_HZ
+    srch = dict(kind="cp_search", x=rx, est=est, n_fft=np.int64(2048), cp_len=np.int64(512),
+                fs=np.float64(fs))
+    srch["robust"] = np.array([core.estimate_cfo_from_cp_robust(rx, int(e), 2048, 512, fs) for e in est])
+    srch["robust_s40_w100"] = np.array([core.estimate_cfo_from_cp_robust(rx, int(e), 2048, 512, fs, span=40,
+                                                                          win_len=100) for e in est])
+    srch["robust_1br_s0"] = np.array([core.estimate_cfo_from_cp_robust(rx[0], int(e), 2048, 512, fs, span=0)
+                                      for e in est])
+    pk = [core.estimate_cfo_from_cp_peak_with_index(rx, int(e), 2048, 512, fs) for e in est]
+    srch["peak_cfo"] = np.array([p[0] for p in pk])
+    srch["peak_d"] = np.array([p[1] for p in pk], np.int64)
+    srch["peak_only"] = np.array([core.estimate_cfo_from_cp_peak(rx, int(e), 2048, 512, fs) for e in est])
+    pk = [core.estimate_cfo_from_cp_peak_with_index(rx[1], int(e), 2048, 256, fs, span=300) for e in est]
+    srch["peak_1br_s300_cfo"] = np.array([p[0] for p in pk])
+    srch["peak_1br_s300_d"] = np.array([p[1] for p in pk], np.int64)
+    srch["find_start"] = np.array([core.find_cp_start_via_corr(rx, int(e), 2048, 512) for e in est], np.int64)
+    srch["find_start_h64"] = np.array([core.find_cp_start_via_corr(rx, int(e), 2048, 512, search_half=64)
+                                       for e in est], np.int64)
+    cases["cp_search"] = srch
 
 
 def gen_park(R, cases):
@@ -413,7 +435,10 @@ def main():
     gen_zc(R, cases)
     gen_post(R, cases)
     OUT.mkdir(parents=True, exist_ok=True)
+    only = set(sys.argv[1:])               # optional case names: rewrite only those files
     for name, d in cases.items():
+        if only and name not in only:
+            continue
         arrs = {k: (np.asarray(v) if not isinstance(v, str) else np.array(v)) for k, v in d.items()}
         np.savez_compressed(OUT / f"{name}.npz", **arrs)
     (OUT / "MANIFEST.txt").write_text(

@@ -73,6 +73,10 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ofs_minn_rtl(0, 1, 1, 1, 16, 0, 3, 0, 3276, 15, 1, None, None, 1, None, None,
                             None, None, 0, 2, 0, 0, None, None, None, None) == -1
     assert lib.ofs_cp_cfo(0, 1, 1, 1, 16, None, 8, 4, 1.0, None, None, None) == -1
+    # cp search: null est, zero window, bad mode
+    assert lib.ofs_cp_search(0, 1, 1, 1, 16, None, 8, 4, 2, 0, 1.0, None, None, 1, 1, None) == -1
+    assert lib.ofs_cp_search(0, 1, 1, 1, 16, 1, 8, 0, 2, 0, 1.0, None, None, 1, 1, None) == -1
+    assert lib.ofs_cp_search(0, 1, 1, 1, 16, 1, 8, 4, 2, 5, 1.0, None, None, 1, 1, None) == -1
     assert lib.ofs_minn_rtl_gate(None, None, None, 1, 16, 2, 0, 1, None, None, None, None) == -1
     # empty batches are valid no-ops
     assert lib.ofs_sc_metric(0, 1, 0, 1, 16, 8, 0, 0, None, None, None, None) == 0

@@ -351,6 +351,58 @@ def test_cp_cfo_vs_reference_golden():
     assert np.allclose(c.cpu().numpy(), d["cfo"], rtol=0, atol=1e-9)
 
 
+def test_cp_search_vs_reference_golden():
+    """core.py:199-336 searches: CFO within 1e-8 Hz, indices exact, fallbacks as the reference."""
+    d = G("cp_search")
+    x, N, cp, fs = d["x"], int(d["n_fft"]), int(d["cp_len"]), float(d["fs"])
+    est = [int(e) for e in d["est"]]
+    close = lambda a, b: np.allclose(a, b, rtol=0, atol=1e-8)   # noqa: E731
+    assert close([core.estimate_cfo_from_cp_robust(x, e, N, cp, fs) for e in est], d["robust"])
+    assert close([core.estimate_cfo_from_cp_robust(x, e, N, cp, fs, span=40, win_len=100) for e in est],
+                 d["robust_s40_w100"])
+    assert close([core.estimate_cfo_from_cp_robust(x[0], e, N, cp, fs, span=0) for e in est], d["robust_1br_s0"])
+    pk = [core.estimate_cfo_from_cp_peak_with_index(x, e, N, cp, fs) for e in est]
+    assert close([p[0] for p in pk], d["peak_cfo"]) and [p[1] for p in pk] == list(d["peak_d"])
+    assert close([core.estimate_cfo_from_cp_peak(x, e, N, cp, fs) for e in est], d["peak_only"])
+    pk = [core.estimate_cfo_from_cp_peak_with_index(x[1], e, N, 256, fs, span=300) for e in est]
+    assert close([p[0] for p in pk], d["peak_1br_s300_cfo"]) and [p[1] for p in pk] == list(d["peak_1br_s300_d"])
+    assert [core.find_cp_start_via_corr(x, e, N, cp) for e in est] == list(d["find_start"])
+    assert [core.find_cp_start_via_corr(x, e, N, cp, search_half=64) for e in est] == list(d["find_start_h64"])
+
+
+@pytest.mark.parametrize("fmt", ["c64", "c128", "int16"])
+def test_cp_search_batched_vs_oracle(fmt):
+    """Batched search over many streams and input formats against the oracle loops."""
+    rng = np.random.default_rng(3)
+    B, nb, T, N, cp = 24, 2, 1500, 512, 128
+    x = (rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))) * 200
+    x[:, :, 700:700 + cp] += x[:, :, 700 + N:700 + N + cp]          # a CP-like repeat per stream
+    x = np.round(x)
+    est = rng.integers(0, T, B)
+    est[:3] = (0, T - N - cp, T - 1)
+    if fmt == "int16":
+        xi = np.stack([x.real, x.imag], -1).astype(np.int16)
+        xd = torch.from_numpy(xi).cuda()
+    else:
+        xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
+    xr = x.astype(np.complex64).astype(np.complex128) if fmt == "c64" else x
+    for mode, win, span in ((core.CPS_ROBUST, 64, 40), (core.CPS_PEAK, cp, 200)):
+        cfo, d, _, st = core.cp_search_batched(xd, est, N, win, span, mode, 1e6)
+        cfo, d, st = cfo.cpu().numpy(), d.cpu().numpy(), st.cpu().numpy()
+        for b in range(B):
+            lo, hi = max(0, est[b] - span), min(T - (N + win), est[b] + span)
+            assert st[b] == (1 if hi <= lo else 0)
+            if st[b]:
+                assert d[b] == est[b]
+                continue
+            if mode == core.CPS_ROBUST:
+                ref = O.cp_cfo_robust(xr[b], int(est[b]), N, 2 * win, 1e6, span=span, win_len=win)
+                assert abs(cfo[b] - ref) < 1e-6
+            else:
+                rc, rd = O.cp_cfo_peak(xr[b], int(est[b]), N, win, 1e6, span=span)
+                assert d[b] == rd and abs(cfo[b] - rc) < 1e-6
+
+
 # ------------------------------------------------------- full-size (BASELINE cfg3) ------------
 def test_aa_fp32_full_batch_properties():
     """B = 65536 streams x T = 1024 c64, L = 512: oracle on a sample of streams, invariants

@@ -71,6 +71,20 @@ def test_oracle_matches_reference_golden(path):
         assert np.allclose(c, d["cfo"], rtol=0, atol=1e-9)
         c1 = [O.cp_cfo(d["x"][0], int(s), 2048, 256, float(d["fs_1br"]))[0] for s in d["starts"]]
         assert np.allclose(c1, d["cfo_1br_cp256"], rtol=0, atol=1e-9)
+    elif kind == "cp_search":
+        x, N, cp, fs = d["x"], int(d["n_fft"]), int(d["cp_len"]), float(d["fs"])
+        est = [int(e) for e in d["est"]]
+        close = lambda a, b: np.allclose(a, b, rtol=0, atol=1e-8)   # noqa: E731
+        assert close([O.cp_cfo_robust(x, e, N, cp, fs) for e in est], d["robust"])
+        assert close([O.cp_cfo_robust(x, e, N, cp, fs, span=40, win_len=100) for e in est], d["robust_s40_w100"])
+        assert close([O.cp_cfo_robust(x[0], e, N, cp, fs, span=0) for e in est], d["robust_1br_s0"])
+        pk = [O.cp_cfo_peak(x, e, N, cp, fs) for e in est]
+        assert close([p[0] for p in pk], d["peak_cfo"]) and close([p[0] for p in pk], d["peak_only"])
+        assert [p[1] for p in pk] == list(d["peak_d"])
+        pk = [O.cp_cfo_peak(x[1], e, N, 256, fs, span=300) for e in est]
+        assert close([p[0] for p in pk], d["peak_1br_s300_cfo"]) and [p[1] for p in pk] == list(d["peak_1br_s300_d"])
+        assert [O.find_cp_start(x, e, N, cp) for e in est] == list(d["find_start"])
+        assert [O.find_cp_start(x, e, N, cp, search_half=64) for e in est] == list(d["find_start_h64"])
     elif kind == "park":
         ds, M, P, E = O.park_metric(d["x"], int(d["N"]))
         assert np.array_equal(ds, d["ds"])
