@@ -48,7 +48,11 @@ struct AaRowGate {
                 double* er = evr + (int64_t)n_ev * 4;
                 ei[0] = bidx; ei[1] = ev_start; ei[2] = gate_end; ei[3] = (int64_t)bidx - 2 * L + 1;
                 er[0] = bpr; er[1] = bpi; er[2] = bm;
-                er[3] = atan2((double)bpi, (double)bpr) * fs / (2.0 * M_PI * (double)L);
+                // fp32 values: fp32 atan2 (P itself carries ~1e-6 relative error; the fp64 ocml
+                // atan2 is ~250 VALU per event), fp64 values: atan2
+                const double ang = sizeof(V) == 4 ? (double)fast_atan2f((float)bpi, (float)bpr)
+                                                  : atan2((double)bpi, (double)bpr);
+                er[3] = ang * fs / (2.0 * M_PI * (double)L);
             }
         }
         n_ev += 1;

@@ -63,10 +63,27 @@ __device__ __forceinline__ float readlane(float v, int j) {
 }
 __device__ __forceinline__ int readlane(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
 
+// full wave64 reductions by a DPP ladder (row_shr 1/2/4/8, row_bcast 15/31): lanes without a
+// source keep the identity (bound_ctrl off, old = identity); the result is read from lane 63
+template <int CTRL, int RMASK = 0xf>
+__device__ __forceinline__ int dpp_old(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, RMASK, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ int dpp_reduce_bits(int v, int ident, Op op) {
+    v = op(v, dpp_old<0x111>(ident, v));
+    v = op(v, dpp_old<0x112>(ident, v));
+    v = op(v, dpp_old<0x114>(ident, v));
+    v = op(v, dpp_old<0x118>(ident, v));
+    v = op(v, dpp_old<0x142, 0xa>(ident, v));
+    v = op(v, dpp_old<0x143, 0xc>(ident, v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
+    const int r = dpp_reduce_bits(__float_as_int(v), __float_as_int(-__builtin_huge_valf()), [](int a, int b) {
+        return __float_as_int(fmaxf(__int_as_float(a), __int_as_float(b)));
+    });
+    return __int_as_float(r);
 }
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -74,14 +91,32 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 __device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-    return v;
+    return dpp_reduce_bits(v, INT32_MIN, [](int a, int b) { return max(a, b); });
 }
 __device__ __forceinline__ int wave_min(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-    return v;
+    return dpp_reduce_bits(v, INT32_MAX, [](int a, int b) { return min(a, b); });
+}
+
+// atan2 in fp32 to ~1.5e-7 rad: odd degree-15 polynomial on [0, 1] (fitted to atan, fp32
+// coefficients) plus octant reduction; ~25 VALU instead of ocml's ~125.  Used where the inputs
+// are fp32 results anyway (the fast path's CFO from an fp32 P).
+__device__ __forceinline__ float fast_atan2f(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float a = mx > 0.f ? mn * __builtin_amdgcn_rcpf(mx) : 0.f;
+    const float s = a * a;
+    float r = -0.004054530523717403f;
+    r = fmaf(r, s, 0.02186284027993679f);
+    r = fmaf(r, s, -0.055912185460329056f);
+    r = fmaf(r, s, 0.09642189741134644f);
+    r = fmaf(r, s, -0.1390862762928009f);
+    r = fmaf(r, s, 0.19946566224098206f);
+    r = fmaf(r, s, -0.33329859375953674f);
+    r = fmaf(r, s, 0.9999993443489075f);
+    r *= a;
+    if (ay > ax) r = 1.5707963267948966f - r;
+    if (x < 0.f) r = 3.141592653589793f - r;
+    return __builtin_copysignf(r, y);
 }
 
 // zero-filled DPP move (bound_ctrl): lanes without a source read 0

@@ -1,0 +1,65 @@
+"""A/B timing of the headline kernel (ofs_aa_detect, cfg3 shape) with parts switched off, to
+see where the time goes: events on/off, outputs stored or not.  Diagnostic only.
+
+    OFS_LIB=build/libofdmsync_x.so python tools/aa_ab.py [--steps K]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
+
+import torch  # noqa: E402
+
+from ofdm_sync_amd import _lib, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--B", type=int, default=65536)
+    ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--L", type=int, default=512)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, T, L, E = a.B, a.T, a.L, 4
+    x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)
+    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
+    R = torch.empty((B, T), dtype=torch.float32, device=dev)
+    M = torch.empty((B, T), dtype=torch.float32, device=dev)
+    n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    lib = _lib.lib()
+    st = torch.cuda.current_stream(dev)
+    lib_name = os.path.basename(os.environ.get("OFS_LIB", "default"))
+    for name, det, outs in (("full", 1, True), ("no_events", 0, True), ("no_outputs", 1, False),
+                            ("read_only", 0, False), ("full_again", 1, True)):
+        p = (P.data_ptr(), R.data_ptr(), M.data_ptr()) if outs else (None, None, None)
+        args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, *p, None, det, 0.15, 128, 15.36e6, E,
+                n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+        fn = lib.ofs_aa_detect
+        for _ in range(a.warmup):
+            fn(*args)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.steps):
+            rc = fn(*args)
+        e1.record(st)
+        torch.cuda.synchronize()
+        if rc:
+            raise RuntimeError(rc)
+        ms = e0.elapsed_time(e1) / a.steps
+        nbytes = B * T * (24 if outs else 8)
+        print(json.dumps({"lib": lib_name, "case": name, "ms": round(ms, 5),
+                          "GBs": round(nbytes / ms / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
