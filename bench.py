@@ -37,8 +37,8 @@ BYTES_PER_EVENT = 64               # 4 x int64 + 4 x f64
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=65536, help="streams per GPU")
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--L", type=int, default=512)
@@ -79,7 +79,7 @@ def cpu_baseline(x_dev: torch.Tensor, L: int, threads: int, gpu_M: torch.Tensor)
 def kernel_label(plan: int) -> str:
     if plan >= 1000:
         e, mr = (plan - 1000) // 10, (plan - 1000) % 10
-        return f"aa_fast_kernel<E={e},MR={mr}> (wave per stream, LDS-DMA staged, fused metric + events)"
+        return f"aa_fast_kernel<E={e},MR={mr}> (wave per stream, register-staged, fused metric + events)"
     return {1: "win_kernel<C64,fp32,AA> (fused events)", 2: "win_kernel<C64,fp32,AA> + aa_events_kernel"}.get(plan, str(plan))
 
 
@@ -105,10 +105,12 @@ def main():
 
     # weak scaling: every rank owns its own B-stream shard (independent streams)
     B, T, L, E = a.batch, a.T, a.L, a.max_events
-    x = synth.make_aa_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev)
-    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
-    R = torch.empty((B, T), dtype=torch.float32, device=dev)
-    M = torch.empty((B, T), dtype=torch.float32, device=dev)
+    # input and outputs of one batch live in ONE device allocation (_lib.arena);
+    # the synthetic batch is generated, then copied in
+    x, P, R, M = _lib.arena(dev, [((B, 1, T), torch.complex64), ((B, T), torch.complex64),
+                                  ((B, T), torch.float32), ((B, T), torch.float32)])
+    x.copy_(synth.make_aa_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev))
+    torch.cuda.empty_cache()
     n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
     ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
     ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)

@@ -46,6 +46,10 @@ constexpr int TMAX = 1024;        // stream length handled by the fast path
 #ifndef OFS_DMA_AUX
 #define OFS_DMA_AUX 0
 #endif
+// stream staging: 0 = LDS-DMA (global_load_lds_dwordx4), 1 = registers
+#ifndef OFS_FAST_STAGE
+#define OFS_FAST_STAGE 1
+#endif
 typedef float nf4 __attribute__((ext_vector_type(4)));
 typedef float nf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_out(float4* p, float4 v) {
@@ -64,10 +68,12 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 }
 
 
-// Stream staging: the wave DMAs its whole stream into a private 8 KiB LDS slice
-// (global_load_lds_dwordx4: no VGPRs, one contiguous 1 KiB per wave-instruction) and reads
-// rows back with conflict-free ds_read_b128 when it needs them — the current row and the row
-// MR back for the lagged product — so samples never occupy registers across rows.
+// Stream staging (OFS_FAST_STAGE): 1 (default) = every row of the lane's samples is loaded into
+// registers up front, each row's first use waits only for its own loads; 0 = the wave DMAs its
+// stream into a private 8 KiB LDS slice (global_load_lds_dwordx4) and reads rows back with
+// ds_read_b128.  Paired A/B on the same buffers: registers 1-3 % faster (profiles/
+// r01c_staging_ab.log; the SOL probe shows the same 8 % gap between LDS-DMA and register staging
+// of this read/write pattern).
 template <int E, int MR>
 __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;                 // samples per row
@@ -75,12 +81,15 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int L = MR * RL;
     constexpr int V4 = E / 2;                  // float4 (2 samples) per lane per row
     static_assert(MR >= 1 && MR <= RW, "window must fit the stream tile");
+#if OFS_FAST_STAGE == 0
     __shared__ float4 lds[FAST_WG / 64][RW * V4][64];
+#endif
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)blockIdx.x * (FAST_WG / 64) + w;
+    const int64_t b = (int64_t)xcd_block() * (FAST_WG / 64) + w;
     if (b >= a.B) return;
     const int T = (int)a.T;
+#if OFS_FAST_STAGE == 0
     {
         const float2* xs = reinterpret_cast<const float2*>(a.x) + b * a.T;
 #pragma unroll
@@ -94,11 +103,29 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                                                  16, 0, OFS_DMA_AUX);
             }
     }
+    auto ldrow = [&](int k, int j) { return lds[w][k * V4 + j][lane]; };
+#else
+    // register staging: every row of the lane's samples is loaded up front (RW * V4 float4), each
+    // row's first use waits only for its own loads (vmcnt counts in order)
+    float4 xreg[RW][V4];
+    {
+        const float2* xs = reinterpret_cast<const float2*>(a.x) + b * a.T;
+#pragma unroll
+        for (int k = 0; k < RW; ++k)
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                int n = RL * k + E * lane + 2 * j;
+                n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
+                xreg[k][j] = *reinterpret_cast<const float4*>(xs + n);
+            }
+    }
+    auto ldrow = [&](int k, int j) { return xreg[k][j]; };
+#endif
     auto xrow = [&](int k, float (&re)[E], float (&im)[E]) {
 #pragma unroll
         for (int j = 0; j < V4; ++j) {
             const bool ok = RL * k + E * lane + 2 * j < T;
-            const float4 v = lds[w][k * V4 + j][lane];
+            const float4 v = ldrow(k, j);
             re[2 * j] = ok ? v.x : 0.f; im[2 * j] = ok ? v.y : 0.f;
             re[2 * j + 1] = ok ? v.z : 0.f; im[2 * j + 1] = ok ? v.w : 0.f;
         }

@@ -97,6 +97,24 @@ __device__ __forceinline__ int wave_min(int v) {
     return dpp_reduce_bits(v, INT32_MAX, [](int a, int b) { return min(a, b); });
 }
 
+// XCD-aware block order.  The dispatcher deals workgroups round-robin over the 8 XCDs (each
+// with its own L2 and TLB), so consecutive blockIdx land on different XCDs.  Remapped, XCD x
+// walks the contiguous block range [x·n/8, (x+1)·n/8) in order: each XCD streams through
+// one compact region of every buffer instead of touching pages all over them.  Identity when
+// the grid is not a multiple of 8 (OFS_XCD_REMAP=0 at build time disables it for A/B).
+#ifndef OFS_XCD_REMAP
+#define OFS_XCD_REMAP 0
+#endif
+__device__ __forceinline__ unsigned xcd_block() {
+#if OFS_XCD_REMAP
+    const unsigned n = gridDim.x, b = blockIdx.x;
+    if ((n & 7u) == 0u) return (b & 7u) * (n >> 3) + (b >> 3);
+    return b;
+#else
+    return blockIdx.x;
+#endif
+}
+
 // atan2 in fp32 to ~1.5e-7 rad: odd degree-15 polynomial on [0, 1] (fitted to atan, fp32
 // coefficients) plus octant reduction; ~25 VALU instead of ocml's ~125.  Used where the inputs
 // are fp32 results anyway (the fast path's CFO from an fp32 P).

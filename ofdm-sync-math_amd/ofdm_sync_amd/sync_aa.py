@@ -81,10 +81,11 @@ def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_ra
          prec: int, want=("P", "R", "M", "valid"), detect: bool = True, max_events: int = 16):
     dev = batch.data.device
     B, T = batch.B, batch.T
-    P = _lib.out_cplx((B, T), prec, dev) if "P" in want else None
-    R = _lib.out_real((B, T), prec, dev) if "R" in want else None
-    M = _lib.out_real((B, T), prec, dev) if "M" in want else None
-    V = torch.empty((B, T), dtype=torch.bool, device=dev) if "valid" in want else None
+    ct = torch.complex128 if prec == _lib.FP64 else torch.complex64
+    rt = torch.float64 if prec == _lib.FP64 else torch.float32
+    P, R, M, V = _lib.arena(dev, [((B, T), ct) if "P" in want else None, ((B, T), rt) if "R" in want else None,
+                                  ((B, T), rt) if "M" in want else None,
+                                  ((B, T), torch.bool) if "valid" in want else None])
     n_ev = ev_i = ev_r = None
     if detect:
         n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)

@@ -25,7 +25,12 @@ def main():
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--L", type=int, default=512)
+    ap.add_argument("--realloc", type=int, default=0, help="only the full case, re-allocating all buffers N times")
+    ap.add_argument("--same", action="store_true", help="realloc sweep without re-allocating (time variation)")
+    ap.add_argument("--libs", default="", help="comma list of library paths timed on the same buffers (realloc)")
     a = ap.parse_args()
+    if a.realloc:
+        return realloc_sweep(a)
     dev = torch.device("cuda", 0)
     B, T, L, E = a.B, a.T, a.L, 4
     x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)
@@ -59,6 +64,56 @@ def main():
         nbytes = B * T * (24 if outs else 8)
         print(json.dumps({"lib": lib_name, "case": name, "ms": round(ms, 5),
                           "GBs": round(nbytes / ms / 1e6, 1)}), flush=True)
+
+
+def realloc_sweep(a):
+    """Same launch, fresh buffers each round: separates allocation (physical placement) effects
+    from code effects."""
+    dev = torch.device("cuda", 0)
+    B, T, L, E = a.B, a.T, a.L, 4
+    import ctypes
+    libs = []
+    for path in (a.libs.split(",") if a.libs else [_lib.LIB_PATH]):
+        l = ctypes.CDLL(os.path.abspath(path))
+        _lib._declare(l)
+        libs.append((os.path.basename(path), l))
+    st = torch.cuda.current_stream(dev)
+    keep = []
+    for r in range(a.realloc):
+        if a.same and keep:
+            x, P, R, M = keep[0]
+            keep.append(keep[0])
+            n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
+        else:
+            if r % 2 == 1:                       # odd rounds: one arena (bench.py layout)
+                x, P, R, M = _lib.arena(dev, [((B, 1, T), torch.complex64), ((B, T), torch.complex64),
+                                              ((B, T), torch.float32), ((B, T), torch.float32)])
+                x.copy_(synth.make_aa_batch(B, T, L, seed=2026, device=dev))
+            else:
+                x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)
+                P = torch.empty((B, T), dtype=torch.complex64, device=dev)
+                R = torch.empty((B, T), dtype=torch.float32, device=dev)
+                M = torch.empty((B, T), dtype=torch.float32, device=dev)
+            n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
+            ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+            ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+        args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
+                0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+        res = {}
+        for name, lib in libs:
+            for _ in range(a.warmup):
+                lib.ofs_aa_detect(*args)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.steps):
+                lib.ofs_aa_detect(*args)
+            e1.record(st)
+            torch.cuda.synchronize()
+            res[name] = round(e0.elapsed_time(e1) / a.steps, 5)
+        print(json.dumps({"round": r, "ms": res, "x": hex(x.data_ptr()), "P": hex(P.data_ptr())}), flush=True)
+        if not a.same or len(keep) == 0:
+            keep.append((x, P, R, M))             # hold: the next round gets new physical pages
 
 
 if __name__ == "__main__":

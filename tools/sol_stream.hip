@@ -61,6 +61,40 @@ __global__ __launch_bounds__(256) void pattern_wave(const float4* __restrict__ x
     }
 }
 
+// pattern_wave with the headline kernel's shape of a wave's life: the stream DMA'd into LDS
+// (global_load_lds_dwordx4), then per row a dependent VALU chain of NV ops (standing in for the
+// metric arithmetic) before the row's stores
+template <int T, int NV>
+__global__ __launch_bounds__(256) void pattern_lds(const float4* __restrict__ x, float4* __restrict__ P,
+                                                   float4* __restrict__ R, float4* __restrict__ M, int64_t B) {
+    constexpr int RW = T / 256;
+    __shared__ float4 lds[4][RW * 2][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * 4 + w;
+    if (b >= B) return;
+    const float2* xs = reinterpret_cast<const float2*>(x) + b * T;
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(xs + 256 * k + 4 * lane + 2 * j),
+                                             (__attribute__((address_space(3))) void*)&lds[w][k * 2 + j][0], 16, 0, 0);
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        float4 a = lds[w][2 * k][lane], c = lds[w][2 * k + 1][lane];
+        float acc = a.x;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) acc = fmaf(acc, 0.999f, c.y);
+        a.x += acc * 1e-30f;
+        const int64_t s = b * T + 256 * k + 4 * lane;
+        P[s / 2] = a; P[s / 2 + 1] = c;
+        const float4 r = make_float4(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w, c.x * c.x + c.y * c.y,
+                                     c.z * c.z + c.w * c.w);
+        R[s / 4] = r;
+        M[s / 4] = make_float4(r.x * 0.5f, r.y * 0.5f, r.z * 0.5f, r.w * 0.5f);
+    }
+}
+
 // read-only and write-only streams
 __global__ void read4(const float4* __restrict__ a, float* out, int64_t n4) {
     float s = 0.f;
@@ -127,6 +161,16 @@ int main(int argc, char** argv) {
     report("pattern_flat(8r+16w) grid=full", 24.0 * n,
            time_ms([&] { pattern_flat<<<(unsigned)((n / 4 + 255) / 256), 256>>>(x, P, R, M, n / 4); }, iters));
     report("pattern_wave(8r+16w) wave-per-stream", 24.0 * n,
+           time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    report("pattern_lds<NV=0>", 24.0 * n,
+           time_ms([&] { pattern_lds<1024, 0><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    report("pattern_lds<NV=64>", 24.0 * n,
+           time_ms([&] { pattern_lds<1024, 64><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    report("pattern_lds<NV=256>", 24.0 * n,
+           time_ms([&] { pattern_lds<1024, 256><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    report("pattern_lds<NV=512>", 24.0 * n,
+           time_ms([&] { pattern_lds<1024, 512><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    report("pattern_wave(8r+16w) wave-per-stream again", 24.0 * n,
            time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
     return 0;
 }
