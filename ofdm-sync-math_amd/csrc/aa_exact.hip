@@ -204,41 +204,6 @@ __global__ __launch_bounds__(XW) void aa_exact_kernel(AaFastArgs a) {
 //   metric_valid = i >= 3Q-1                                  (minn_rtl.py:609-643, :691-702)
 // The lagged prefixes (Q, 2Q, 3Q back) live in a per-wave LDS ring of rows.
 // ------------------------------------------------------------------------------------------
-// IIR over one row: positions j < cnt of the row in order (lane j / E, element j % E); the state
-// updates from position vfrom on (metric_valid), holds before.  MODE 0: s += (c - s) / 2^k in
-// float64 (minn_rtl.py:706-715, contraction off: the reference's exact operation sequence);
-// 1: shift 0, s = c; 2: integer floor shift of the RTL (ref/minn_preamble_detector.sv:288-296).
-template <int E, int MODE>
-__device__ __forceinline__ void smooth_row(const double (&c)[E], double (&out)[E], double& sm, long long& si,
-                                           int lane, int cnt, int vfrom, double inv, int shift) {
-#pragma clang fp contract(off)
-    const int jf = vfrom < cnt ? vfrom : cnt;                     // positions before jf: state holds
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-        if (E * lane + e < jf) out[e] = sm;
-    const int l1 = (cnt + E - 1) / E;
-#pragma unroll 2
-    for (int l = jf / E; l < l1; ++l) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int j = E * l + e;
-            if (j >= jf && j < cnt) {
-                const double cj = readlane(c[e], l);
-                if constexpr (MODE == 0) {
-                    sm = sm + (cj - sm) * inv;
-                } else if constexpr (MODE == 1) {
-                    sm = cj;
-                } else {
-                    const long long ci = (long long)cj;
-                    si = (shift == 0) ? ci : si + ((ci - si) >> shift);
-                    sm = (double)si;
-                }
-                if (lane == l) out[e] = sm;
-            }
-        }
-    }
-}
-
 struct RtlExactArgs {
     const void* x; int64_t B, T; int32_t nb, Q;
     int32_t shift, smooth_mode, frac_bits; double thr_value;
@@ -247,11 +212,41 @@ struct RtlExactArgs {
     int32_t detect, hyst, toff, max_ev; int32_t* n_ev; int64_t* ev; int64_t* open_start;
 };
 
-// per-wave LDS ring: prefix rows k-3MW..k of Ae and Ac, and the raw words of rows k-MW..k-1
-// of every branch (lane-private columns: conflict-free, no barriers)
+// ---- segment-parallel smoothing -----------------------------------------------------------
+// The stream is cut into segments of SEG = 64·SC samples; lane j owns the chunk of SC samples
+// [s0 + SC·j, s0 + SC·(j+1)).  The float IIR s <- s + (c - s)·2^-k (minn_rtl.py:706-715) is
+// evaluated EXACTLY - the reference's sequential operation sequence, contraction off - by
+// every lane over its own chunk, from an entering state that is made self-consistent:
+//   1. guess: each lane maps its chunk from s = 0 and records the affine map s_out = A·s_in + Z;
+//      a wave scan of the maps applied to the exact carried state gives every chunk's
+//      entering state to a few ulps;
+//   2. round: every lane runs the exact recursion over its chunk from its entering state; the
+//      chain is consistent when each lane's entering state equals lane j-1's leaving state
+//      bit for bit (lane 0 enters with the exact carried state).  Otherwise every lane takes
+//      lane j-1's leaving state as its new entering state and the round repeats.
+// The recursion is deterministic, so a consistent chain IS the reference's trajectory (by
+// induction from lane 0).  After round r lanes 0..r are exact, so it ends within 64 rounds
+// (the sequential cost); in practice the guessed trajectories coincide with the exact one
+// inside a chunk or two and a segment takes a few rounds.  The integer floor-shift RTL mode
+// (not contractive to the bit) runs sequentially.
+#ifndef OFS_RTL_SC
+#define OFS_RTL_SC 4
+#endif
+constexpr int SC = OFS_RTL_SC;
+constexpr int SEG = 64 * SC;
+constexpr int SEG_PAD = SEG + SEG / SC;                // chunk stride SC + 1 doubles (banks)
+__device__ __forceinline__ int seg_at(int i) { return i + i / SC; }
+
+// per-wave LDS: prefix rows k-3MW..k of Ae and Ac, the raw words of rows k-MW..k-1 of every
+// branch (lane-private columns), the segment's corr_positive and energy_scaled
 __host__ __device__ constexpr int rtl_ring_rows(int MW) { return 3 * MW + 1; }
 __host__ __device__ constexpr size_t rtl_wave_lds(int E, int MW, int nb) {
-    return (size_t)2 * rtl_ring_rows(MW) * E * 64 * sizeof(double) + (size_t)nb * MW * E * 64 * sizeof(int32_t);
+    return (size_t)2 * rtl_ring_rows(MW) * E * 64 * sizeof(double) + (size_t)2 * SEG_PAD * sizeof(double) +
+           (size_t)nb * MW * E * 64 * sizeof(int32_t);
+}
+
+__device__ __forceinline__ bool same_bits(double a, double b) {
+    return __double_as_longlong(a) == __double_as_longlong(b);
 }
 
 template <int E, int MW>
@@ -260,6 +255,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     constexpr int RL = 64 * E;
     constexpr int Q = MW * RL;
     constexpr int NR = rtl_ring_rows(MW);
+    static_assert(SEG % RL == 0, "segment = whole metric rows");
     extern __shared__ __attribute__((aligned(16))) double rsm[];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -270,7 +266,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const int nb_ = a.nb;
     double* hae_ = rsm + (rtl_wave_lds(E, MW, nb_) / sizeof(double)) * w;
     double* hac_ = hae_ + NR * E * 64;
-    int32_t* hx_ = reinterpret_cast<int32_t*>(hac_ + NR * E * 64);
+    double* hcp = hac_ + NR * E * 64;                                // segment corr_positive
+    double* hes = hcp + SEG_PAD;                                     // segment energy_scaled
+    int32_t* hx_ = reinterpret_cast<int32_t*>(hes + SEG_PAD);
     auto hae = [&](int r, int e) -> double& { return hae_[(r * E + e) * 64 + lane]; };
     auto hac = [&](int r, int e) -> double& { return hac_[(r * E + e) * 64 + lane]; };
     auto hx = [&](int t, int m, int e) -> int32_t& { return hx_[((t * MW + m) * E + e) * 64 + lane]; };
@@ -289,13 +287,14 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const int64_t row_off = b * T;
     const int vstart = 3 * Q - 1;
     const double inv = ldexp(1.0, -(a.shift > 0 ? a.shift : 0));   // exact 1 / 2^shift
+    const double keep = 1.0 - inv;
     const double scale = (double)(1ll << a.frac_bits);
     const bool seq = a.smooth || a.corr_scaled || a.above || a.detect;
     const int smode = a.smooth_mode == 1 ? 2 : (a.shift == 0 ? 1 : 0);
     double CC = 0.0, CE = 0.0;
-    double sm = 0.0;                                               // IIR state (wave-uniform)
+    double sm = 0.0;                                               // IIR state carried between segments
     long long si = 0;
-    AaRowGate<E, double, true> gate;                               // detect_minn_rtl, closed form
+    AaRowGate<SC, double, true> gate;                              // detect_minn_rtl, closed form
     if (a.detect)
         gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
                   nullptr, a.toff);
@@ -314,112 +313,214 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 for (int e = 0; e < E; ++e) nx[p][t][e] = 0;
         }
 
-    for (int k = 0; k < nrows; ++k) {
-        const int nb = RL * k + E * lane;
-        const int xsl = k % MW;
-        int32_t cur[NBM][E];
-#pragma unroll
-        for (int t = 0; t < NBM; ++t)
-#pragma unroll
-            for (int e = 0; e < E; ++e) cur[t][e] = nx[0][t][e];
-#pragma unroll
-        for (int p = 0; p + 1 < PD; ++p)
-#pragma unroll
-            for (int t = 0; t < NBM; ++t)
-#pragma unroll
-                for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
-        if (k + PD < nrows) {
+    const int nseg = (int)((T + SEG - 1) / SEG);
+    for (int g = 0; g < nseg; ++g) {
+        const int64_t s0 = (int64_t)SEG * g;
+        const int k0 = g * (SEG / RL), k1 = min(nrows, (g + 1) * (SEG / RL));
+        // ---------------- phase A: metric rows of the segment (stores of the metric arrays) ----
+        for (int k = k0; k < k1; ++k) {
+            const int nb = RL * k + E * lane;
+            const int xsl = k % MW;
+            int32_t cur[NBM][E];
 #pragma unroll
             for (int t = 0; t < NBM; ++t)
-                if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[PD - 1][t]);
-        }
-        double pc[E], en[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
+                for (int e = 0; e < E; ++e) cur[t][e] = nx[0][t][e];
 #pragma unroll
-        for (int t = 0; t < NBM; ++t) {
-            if (t < nb_) {
+            for (int p = 0; p + 1 < PD; ++p)
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int32_t d = hx(t, xsl, e);
-                    const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
-                    pc[e] += w_re(d) * xr + w_im(d) * xi;            // minn_rtl.py:616, exact
-                    en[e] += xr * xr + xi * xi;                       // :617
-                    hx(t, xsl, e) = cur[t][e];
+                for (int t = 0; t < NBM; ++t)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
+            if (k + PD < nrows) {
+#pragma unroll
+                for (int t = 0; t < NBM; ++t)
+                    if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[PD - 1][t]);
+            }
+            double pc[E], en[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
+#pragma unroll
+            for (int t = 0; t < NBM; ++t) {
+                if (t < nb_) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int32_t d = hx(t, xsl, e);
+                        const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
+                        pc[e] += w_re(d) * xr + w_im(d) * xi;            // minn_rtl.py:616, exact
+                        en[e] += xr * xr + xi * xi;                       // :617
+                        hx(t, xsl, e) = cur[t][e];
+                    }
                 }
             }
-        }
-        RowPrefix<E> qc, qe;
-        qc.run(pc); qe.run(en);
-        const int s0 = k % NR;                                         // slot of row k
-        const int s1 = (k + NR - MW) % NR, s2 = (k + NR - 2 * MW) % NR, s3 = (k + NR - 3 * MW) % NR;
-        double ct[E], cpos[E], et[E], es[E];
-        bool mv[E];
+            RowPrefix<E> qc, qe;
+            qc.run(pc); qe.run(en);
+            const int s0r = k % NR;                                        // slot of row k
+            const int s1 = (k + NR - MW) % NR, s2 = (k + NR - 2 * MW) % NR, s3 = (k + NR - 3 * MW) % NR;
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const double c0 = (CC + qc.excl) + qc.f[e];
-            const double e0 = (CE + qe.excl) + qe.f[e];
-            hac(s0, e) = c0;
-            hae(s0, e) = e0;
-            // prefixes before the stream start are 0
-            const double c1 = k >= MW ? hac(s1, e) : 0.0;
-            const double c2 = k >= 2 * MW ? hac(s2, e) : 0.0;
-            const double e1 = k >= MW ? hae(s1, e) : 0.0;
-            const double e2 = k >= 2 * MW ? hae(s2, e) : 0.0;
-            const double e3 = k >= 3 * MW ? hae(s3, e) : 0.0;
-            const int i = nb + e;
-            const double cr_ = (i >= Q - 1) ? c0 - c1 : 0.0;
-            const double cp_ = (i >= 2 * Q - 1) ? c1 - c2 : 0.0;
-            const double er_ = (i >= Q - 1) ? e0 - e1 : 0.0;
-            const double ep_ = (i >= 2 * Q - 1) ? e1 - e2 : 0.0;
-            const double ep2 = (i >= 3 * Q - 1) ? e2 - e3 : 0.0;
-            ct[e] = 0.0 + (cr_ + cp_);                                 // minn_rtl.py:696
-            et[e] = 0.0 + ((er_ + ep_) + ep2);                         // :697-701
-            cpos[e] = ct[e] > 0.0 ? ct[e] : 0.0;                       // :704
-            es[e] = (a.thr_value == 0.0) ? 0.0 : et[e] * a.thr_value;  // :718-721
-            mv[e] = i >= vstart;
+            for (int e = 0; e < E; ++e) {
+                const double c0 = (CC + qc.excl) + qc.f[e];
+                const double e0 = (CE + qe.excl) + qe.f[e];
+                hac(s0r, e) = c0;
+                hae(s0r, e) = e0;
+                // prefixes before the stream start are 0
+                const double c1 = k >= MW ? hac(s1, e) : 0.0;
+                const double c2 = k >= 2 * MW ? hac(s2, e) : 0.0;
+                const double e1 = k >= MW ? hae(s1, e) : 0.0;
+                const double e2 = k >= 2 * MW ? hae(s2, e) : 0.0;
+                const double e3 = k >= 3 * MW ? hae(s3, e) : 0.0;
+                const int i = nb + e;
+                const double cr_ = (i >= Q - 1) ? c0 - c1 : 0.0;
+                const double cp_ = (i >= 2 * Q - 1) ? c1 - c2 : 0.0;
+                const double er_ = (i >= Q - 1) ? e0 - e1 : 0.0;
+                const double ep_ = (i >= 2 * Q - 1) ? e1 - e2 : 0.0;
+                const double ep2 = (i >= 3 * Q - 1) ? e2 - e3 : 0.0;
+                const double ct = 0.0 + (cr_ + cp_);                       // minn_rtl.py:696
+                const double et = 0.0 + ((er_ + ep_) + ep2);               // :697-701
+                const double cpos = ct > 0.0 ? ct : 0.0;                   // :704
+                const double es = (a.thr_value == 0.0) ? 0.0 : et * a.thr_value;   // :718-721
+                const int li = (int)(i - s0);
+                hcp[seg_at(li)] = cpos;
+                hes[seg_at(li)] = es;
+                if (i < T) {
+                    const int64_t gi = row_off + i;
+                    a.corr_total[gi] = ct;
+                    if (a.corr_positive) a.corr_positive[gi] = cpos;
+                    a.energy_total[gi] = et;
+                    if (a.energy_scaled) a.energy_scaled[gi] = es;
+                    if (a.mvalid) a.mvalid[gi] = (uint8_t)(i >= vstart);
+                }
+            }
+            CC += qc.tot; CE += qe.tot;
         }
-        CC += qc.tot; CE += qe.tot;
+        if (!seq) continue;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // smoothing: the reference's sequential recursion over the row's samples, in order, on
-        // wave-uniform values (only the IIR chain is serial); threshold and gate are vector work
-        double smv[E];
-        bool abv[E];
+        // ---------------- phase B: smoothing of the segment, lane j = chunk j ----------------
+        const int64_t c0 = s0 + (int64_t)SC * lane;                   // first sample of my chunk
+        const int64_t send = min(T, s0 + SEG);
+        double own[SC];                                                // smoothed, my chunk
+        int fail_from = 64;                                            // first chunk to redo serially
+        if (smode == 1) {                                              // shift 0: s = c (no chain)
 #pragma unroll
-        for (int e = 0; e < E; ++e) { smv[e] = 0.0; abv[e] = false; }
-        if (seq) {
-            const int64_t r0 = (int64_t)RL * k;
-            const int cnt = (int)min((int64_t)RL, T - r0);
-            const int vfrom = (int)max((int64_t)0, min((int64_t)cnt, (int64_t)vstart - r0));
-            if (smode == 0) smooth_row<E, 0>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
-            else if (smode == 1) smooth_row<E, 1>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
-            else smooth_row<E, 2>(cpos, smv, sm, si, lane, cnt, vfrom, inv, a.shift);
+            for (int e = 0; e < SC; ++e) {
+                const int64_t p = c0 + e;
+                own[e] = (p >= vstart && p < T) ? hcp[seg_at(SC * lane + e)] : 0.0;
+            }
+            // state holds where invalid (before vstart: the initial 0); positions >= T unused
+            if (send - 1 >= vstart) sm = hcp[seg_at((int)(send - 1 - s0))];
+        } else if (smode == 0) {
+            // 1. chunk maps from s = 0: s_out = A·s_in + Z (approximate arithmetic is fine here)
+            double A = 1.0, Z = 0.0;
 #pragma unroll
-            for (int e = 0; e < E; ++e)
-                abv[e] = mv[e] && nb + e < T && (smv[e] * scale >= es[e]);   // minn_rtl.py:717-722
-            if (a.detect && r0 + cnt > vstart) {
-                double none[E];
+            for (int e = 0; e < SC; ++e) {
+                const int64_t p = c0 + e;
+                if (p >= vstart && p < T) {
+                    const double c = hcp[seg_at(SC * lane + e)];
+                    Z = Z + (c - Z) * inv;
+                    A = A * keep;
+                }
+            }
+            // inclusive wave scan of the affine maps (compose lane-1's map first, then mine)
+            {
+                double sa = A, sz = Z;
 #pragma unroll
-                for (int e = 0; e < E; ++e) none[e] = 0.0;
-                gate.row_flags(lane, k, nb, (int)T, abv, cpos, none, none, none);
+                for (int d = 1; d < 64; d <<= 1) {
+                    const double pa = __shfl_up(sa, d, 64), pz = __shfl_up(sz, d, 64);
+                    if (lane >= d) { sz = sa * pz + sz; sa = sa * pa; }
+                }
+                // entering state of my chunk: exclusive map applied to the carried exact state
+                const double ea = __shfl_up(sa, 1, 64), ez = __shfl_up(sz, 1, 64);
+                double enter = lane == 0 ? sm : ea * sm + ez;
+                // 2./3. exact chunk runs until the chain is self-consistent: every lane runs the
+                // reference recursion over its chunk from `enter`, then takes lane-1's leaving
+                // state as its new `enter`; stop when no lane's entering state changes.  Lane 0
+                // starts exact, and after round r lanes 0..r are exact, so <= 64 rounds.
+                double cv[SC];
+                bool upd[SC];
+#pragma unroll
+                for (int e = 0; e < SC; ++e) {
+                    const int64_t p = c0 + e;
+                    upd[e] = p >= vstart && p < T;
+                    cv[e] = hcp[seg_at(SC * lane + e)];
+                }
+                int round = 0;
+                for (; round <= 64; ++round) {
+                    double st = enter;
+#pragma unroll
+                    for (int e = 0; e < SC; ++e) {
+                        if (upd[e]) st = st + (cv[e] - st) * inv;
+                        own[e] = st;
+                    }
+                    const double up = __shfl_up(st, 1, 64);
+                    const double prev_leave = lane == 0 ? sm : up;
+                    const bool ok = same_bits(enter, prev_leave);
+                    if (__ballot(!ok) == 0) {
+                        sm = readlane(st, 63);
+                        break;
+                    }
+                    enter = prev_leave;
+                }
+#ifdef OFS_RTL_DEBUG
+                if (b < 4 && lane == 0) printf("rtl b=%ld seg=%d rounds=%d\n", (long)b, g, round);
+#endif
+            }
+        } else {
+            fail_from = 0;
+        }
+#ifdef OFS_RTL_DEBUG
+        if (b < 4 && lane == 0) printf("rtl b=%ld seg=%d fail_from=%d shift=%d smode=%d\n", (long)b, g, fail_from,
+                                       a.shift, smode);
+#endif
+        if (fail_from < 64) {
+            // sequential recomputation from chunk fail_from with the exact state (wave-uniform)
+            double sv = fail_from == 0 ? sm : readlane(own[SC - 1], fail_from - 1);
+            long long siv = si;
+            for (int q = fail_from; q < 64; ++q) {
+#pragma unroll
+                for (int e = 0; e < SC; ++e) {
+                    const int64_t p = s0 + (int64_t)SC * q + e;
+                    if (p >= vstart && p < T) {
+                        const double c = hcp[seg_at(SC * q + e)];
+                        if (smode == 0) {
+                            sv = sv + (c - sv) * inv;
+                        } else {                                       // RTL floor shift
+                            const long long ci = (long long)c;
+                            siv = (a.shift == 0) ? ci : siv + ((ci - siv) >> a.shift);
+                            sv = (double)siv;
+                        }
+                    }
+                    if (lane == q) own[e] = sv;
+                }
+            }
+            sm = sv; si = siv;
+        }
+
+        // ---------------- phase C: threshold, gate, stores (chunk layout) ----------------------
+        bool abv[SC];
+        double cp8[SC];
+#pragma unroll
+        for (int e = 0; e < SC; ++e) {
+            const int64_t p = c0 + e;
+            const int at = seg_at(SC * lane + e);
+            cp8[e] = hcp[at];
+            abv[e] = p >= vstart && p < T && (own[e] * scale >= hes[at]);      // minn_rtl.py:717-722
+            if (p < T) {
+                const int64_t gi = row_off + p;
+                if (a.smooth) a.smooth[gi] = own[e];
+                if (a.corr_scaled) a.corr_scaled[gi] = own[e] * scale;
+                if (a.above) a.above[gi] = (uint8_t)abv[e];
             }
         }
-        // stores (lane-consecutive)
+        if (a.detect && send > vstart) {
+            double none[SC];
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int64_t i = nb + e;
-            if (i < T) {
-                const int64_t g = row_off + i;
-                a.corr_total[g] = ct[e];
-                if (a.corr_positive) a.corr_positive[g] = cpos[e];
-                a.energy_total[g] = et[e];
-                if (a.energy_scaled) a.energy_scaled[g] = es[e];
-                if (a.mvalid) a.mvalid[g] = (uint8_t)mv[e];
-                if (a.smooth) a.smooth[g] = smv[e];
-                if (a.corr_scaled) a.corr_scaled[g] = smv[e] * scale;
-                if (a.above) a.above[g] = (uint8_t)abv[e];
-            }
+            for (int e = 0; e < SC; ++e) none[e] = 0.0;
+            gate.row_flags(lane, g, (int)c0, (int)T, abv, cp8, none, none, none);
         }
+        __builtin_amdgcn_wave_barrier();                               // LDS reuse by the next segment
     }
     if (a.detect) gate.finish(lane, (int)T, a.n_ev + b, a.open_start ? a.open_start + b : nullptr);
 }
@@ -458,6 +559,8 @@ template <int E, int MW>
 int rtl_launch(const RtlExactArgs& a, hipStream_t st) {
     const size_t per_wave = rtl_wave_lds(E, MW, a.nb);
     int wpb = 4;                                             // waves (streams) per workgroup
+    const char* ev = getenv("OFS_RTL_WPB");                  // tuning: 1, 2 or 4
+    if (ev && (atoi(ev) == 1 || atoi(ev) == 2)) wpb = atoi(ev);
     while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
     const size_t lds = per_wave * wpb;
     auto k = rtl_exact_kernel<E, MW>;
@@ -508,6 +611,7 @@ int ofs_rtl_exact_try(int fmt, int n_br, const RtlExactCall& c, hipStream_t st) 
     a.energy_total = c.energy_total; a.corr_scaled = c.corr_scaled; a.energy_scaled = c.energy_scaled;
     a.mvalid = c.mvalid; a.above = c.above; a.detect = c.detect; a.hyst = c.hyst; a.toff = c.toff;
     a.max_ev = c.max_ev; a.n_ev = c.n_ev; a.ev = c.ev; a.open_start = c.open_start;
+
     switch (plan) {
         case 11: return rtl_launch<1, 1>(a, st);
         case 12: return rtl_launch<1, 2>(a, st);

@@ -130,3 +130,25 @@ def test_exact_plans_fall_back_outside_exact_range():
     assert L_.ofs_aa_plan(_lib.CI16, _lib.FP64, 1, (1 << 21) + 2, 128) < 2000  # sums may pass 2^53
     assert L_.ofs_rtl_plan(_lib.CI16, 1, 1024, 1024) == 0                     # Q > 512
     assert L_.ofs_rtl_plan(_lib.C128, 1, 1024, 64) == 0
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("T", [1024, 2100, 513])
+def test_rtl_segment_parallel_iir_is_exact(shift, T, monkeypatch):
+    """The segment-parallel IIR (aa_exact.hip: guessed chunk states, exact chunk runs iterated
+    to a self-consistent chain) equals the general engine's sequential recursion and the
+    oracle bit for bit, across contraction factors and partial segments."""
+    rng = np.random.default_rng(100 + shift + T)
+    B, nb, Q = 9, 2, 64
+    iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q)))
+    xt = torch.from_numpy(iq).cuda()
+    kw = dict(smooth_shift=shift, threshold_value=3276, threshold_frac_bits=15, smooth_mode="float",
+              hysteresis=2, timing_offset=0)
+    a = _rtl_run(xt, Q, monkeypatch, True, **kw)
+    g = _rtl_run(xt, Q, monkeypatch, False, **kw)
+    for k in RTL_KEYS + ("n_events", "open_gate_start"):
+        assert torch.equal(getattr(a, k), getattr(g, k)), k
+    xc = (iq[1, ..., 0] + 1j * iq[1, ..., 1]).astype(np.complex128)
+    s = O.minn_rtl_metric(xc, Q, shift, 3276, 15)
+    for k in RTL_KEYS:
+        assert np.array_equal(getattr(a, k)[1].cpu().numpy(), s[k]), k
