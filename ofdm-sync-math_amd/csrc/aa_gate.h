@@ -39,20 +39,28 @@ struct AaRowGate {
         bpm = (V)-1; bpr = (V)0; bpi = (V)0; bm = (V)0;
     }
 
+    // the record is wave-uniform: lanes 0..3 store the four int64 fields and lanes 4..7 the four
+    // f64 fields, one store instruction per 32-byte record half (a lane-0 loop of 8-byte stores
+    // cost ~450 B of write traffic per event, measured with WRITE_SIZE)
     __device__ __forceinline__ void emit(int lane, int gate_end) {
-        if (lane == 0 && evi && n_ev < max_ev) {
+        if (evi && n_ev < max_ev && lane < 8) {
             int64_t* ei = evi + (int64_t)n_ev * 4;
             if constexpr (RTL) {
-                ei[0] = bidx; ei[1] = (int64_t)bidx + toff; ei[2] = ev_start; ei[3] = (int64_t)gate_end + 1;
+                const int64_t f[4] = {bidx, (int64_t)bidx + toff, ev_start, (int64_t)gate_end + 1};
+                if (lane < 4) ei[lane] = f[lane & 3];
             } else {
                 double* er = evr + (int64_t)n_ev * 4;
-                ei[0] = bidx; ei[1] = ev_start; ei[2] = gate_end; ei[3] = (int64_t)bidx - 2 * L + 1;
-                er[0] = bpr; er[1] = bpi; er[2] = bm;
-                // fp32 values: fp32 atan2 (P itself carries ~1e-6 relative error; the fp64 ocml
-                // atan2 is ~250 VALU per event), fp64 values: atan2
-                const double ang = sizeof(V) == 4 ? (double)fast_atan2f((float)bpi, (float)bpr)
-                                                  : atan2((double)bpi, (double)bpr);
-                er[3] = ang * fs / (2.0 * M_PI * (double)L);
+                const int64_t f[4] = {bidx, ev_start, gate_end, (int64_t)bidx - 2 * L + 1};
+                if (lane < 4) {
+                    ei[lane] = f[lane & 3];
+                } else {
+                    // fp32 values: fp32 atan2 (P itself carries ~1e-6 relative error; the fp64 ocml
+                    // atan2 is ~250 VALU per event), fp64 values: atan2
+                    const double ang = sizeof(V) == 4 ? (double)fast_atan2f((float)bpi, (float)bpr)
+                                                      : atan2((double)bpi, (double)bpr);
+                    const double g[4] = {(double)bpr, (double)bpi, (double)bm, ang * fs / (2.0 * M_PI * (double)L)};
+                    er[lane - 4] = g[lane & 3];
+                }
             }
         }
         n_ev += 1;
