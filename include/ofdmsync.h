@@ -191,6 +191,28 @@ int32_t ofs_cp_search(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, in
                       double* cfo_out, int32_t* status, void* stream);
 
 /*
+ * Receiver back-end after sync, batched over frames: the chain of sc.run_simulation
+ * (sc.py:274-311) over core.py helpers - estimate_cfo_from_cp (core.py:179-196, skipped when
+ * cfo_in is given), apply_cfo(-cfo) (:123-138) + branch mean, ofdm_fft_used (:171-176),
+ * ls_channel_estimate (:339-341), estimate_timing_offset_from_phase_slope (:443-469),
+ * equalize (:344-345), align_complex_gain (:357-362), evm_rms_db (:365-370).  fp64.
+ *   pilot_start / data_start [B] int64: CP start of the pilot / data symbol (device);
+ *   cfo_in [B] f64 or NULL; bins [n_used] int32 (device): centred subcarrier indices k, used
+ *   for the gather X[k mod N] (= fftshift + (N/2 + k) % N) and as the fit's abscissa;
+ *   pilot_used / data_used: c128 [.. ][n_used] known symbols, row stride (elements) per frame
+ *   (0 = one row shared by all frames);  n_fft a power of two <= 4096.
+ * Outputs (device, nullable): cfo_out [B], h_out / xa_out c128 [B][n_used], gain_out c128 [B],
+ * evm_out, evm_db_out, slope_out (rad/bin), sto_out (samples) [B] f64.
+ */
+int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                       int32_t n_fft, int32_t cp_len, double fs_hz, const int64_t* pilot_start,
+                       const int64_t* data_start, const double* cfo_in, int32_t n_used,
+                       const int32_t* bins, const void* pilot_used, int64_t pilot_stride,
+                       const void* data_used, int64_t data_stride, double* cfo_out, void* h_out,
+                       void* xa_out, void* gain_out, double* evm_out, double* evm_db_out,
+                       double* slope_out, double* sto_out, void* stream);
+
+/*
  * Park mirror-symmetry metric: replaces park.park_streaming_metric (park.py:64-114).
  * half = N/2; outputs for d in [half, T-half-1], n_out = T - 2*half, laid out [B][n_out]:
  *   P (c64|c128) = sum_br sum_{k<half} x[d-k]*x[d+k]; E (f32|f64) = sum_br sum_{k<half}|x[d+k]|^2;

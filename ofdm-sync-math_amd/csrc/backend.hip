@@ -1,0 +1,312 @@
+// backend.hip — batched OFDM receiver back-end behind the timing/CFO path (core.py:171-176,
+// :179-196, :339-370, :443-469 as chained by sc.run_simulation, sc.py:274-311):
+//
+//   cfo      = estimate_cfo_from_cp(rx, pilot_start, N, cp, fs)        (or given per frame)
+//   rx_eff   = mean_br( apply_cfo(rx, -cfo, fs) )                       (core.py:123-138)
+//   y_pilot  = ofdm_fft_used(rx_eff[pilot_start + cp : + N])            (core.py:171-176)
+//   h        = ls_channel_estimate(y_pilot, pilot_used)                  (core.py:339-341)
+//   slope, sto = estimate_timing_offset_from_phase_slope(h)             (core.py:443-469)
+//   y_data   = ofdm_fft_used(rx_eff[data_start + cp : + N])
+//   xhat     = equalize(y_data, h)                                       (core.py:344-345)
+//   xa, gain = align_complex_gain(xhat, data_used)                      (core.py:357-362)
+//   evm, db  = evm_rms_db(xa, data_used)                                 (core.py:365-370)
+//
+// One 256-thread workgroup per frame, fp64 throughout (the reference is float64):
+//   * the two N-point DFTs are iterative radix-2 FFTs in LDS (bit-reversed load, twiddles
+//     from sincospi of exact rationals, one table per workgroup), N a power of two <= 4096;
+//   * fftshift + used-bin gather collapse to X[k mod N] for the centred bin indices k;
+//   * np.unwrap is a per-bin correction (numpy's mod / boundary rule) followed by a prefix sum
+//     (block scan), the phase-slope fit and all means are block reductions.
+// Per-frame, O(N log N) work: compute-bound and tiny next to the metric kernels.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include "ofdmsync.h"
+#include "ofs_common.h"
+
+namespace {
+
+constexpr int BW = 256;
+constexpr int BNMAX = 4096;
+
+struct BeArgs {
+    int fmt; const void* x; int64_t T; int nb; int N, cp, n_used; double fs;
+    const int64_t* pilot_start; const int64_t* data_start; const double* cfo_in;
+    const int32_t* bins; const double2* pilot; int64_t pilot_stride; const double2* data; int64_t data_stride;
+    double* cfo_out; double2* h_out; double2* xa_out; double2* gain_out; double* evm_out; double* evm_db_out;
+    double* slope_out; double* sto_out;
+};
+
+template <int FMT>
+__device__ __forceinline__ double2 ld(const void* p, int64_t i) {
+    if constexpr (FMT == OFS_C64) {
+        const float2 v = static_cast<const float2*>(p)[i];
+        return make_double2(v.x, v.y);
+    } else if constexpr (FMT == OFS_C128) {
+        return static_cast<const double2*>(p)[i];
+    } else {
+        const short2 v = static_cast<const short2*>(p)[i];
+        return make_double2(v.x, v.y);
+    }
+}
+
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a / b, Smith's algorithm (scaled; the form numpy's complex division uses)
+__device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
+    if (fabs(b.x) >= fabs(b.y)) {
+        if (b.x == 0.0 && b.y == 0.0) return make_double2(a.x / fabs(b.x), a.y / fabs(b.y));
+        const double r = b.y / b.x, d = b.x + b.y * r;
+        return make_double2((a.x + a.y * r) / d, (a.y - a.x * r) / d);
+    }
+    const double r = b.x / b.y, d = b.y + b.x * r;
+    return make_double2((a.x * r + a.y) / d, (a.y * r - a.x) / d);
+}
+
+// block-wide sum of doubles (all threads get the result)
+__device__ double block_sum(double v, double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < BW / 64; ++k) s += red[k];
+    return s;
+}
+
+// numpy.mod for float64 (result has the sign of the divisor)
+__device__ __forceinline__ double np_mod(double a, double b) {
+    double m = fmod(a, b);
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+
+// N-point forward DFT of buf (natural order in / out) in LDS; tw[j] = exp(-2 pi i j / N)
+__device__ void fft_lds(double2* buf, const double2* tw, int N, int LB) {
+    for (int len = 2; len <= N; len <<= 1) {
+        const int half = len >> 1, step = N / len;
+        for (int j = threadIdx.x; j < N / 2; j += BW) {
+            const int g = j / half, k = j - g * half;
+            const int p = g * len + k, q = p + half;
+            const double2 t = cmul(tw[k * step], buf[q]);
+            const double2 u = buf[p];
+            buf[p] = make_double2(u.x + t.x, u.y + t.y);
+            buf[q] = make_double2(u.x - t.x, u.y - t.y);
+        }
+        __syncthreads();
+    }
+    (void)LB;
+}
+
+__device__ __forceinline__ int bitrev(int v, int bits) { return (int)(__brev((unsigned)v) >> (32 - bits)); }
+
+// load rx_eff[s : s + N] = mean_br(rx[br] * exp(-i 2 pi cfo n / fs)) bit-reversed into buf
+template <int FMT>
+__device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, double2* buf, int LB) {
+    const double w0 = 2.0 * M_PI * (-cfo);
+    for (int n = threadIdx.x; n < a.N; n += BW) {
+        const int64_t i = s + n;
+        double2 acc = make_double2(0.0, 0.0);
+        if (i >= 0 && i < a.T) {
+            // tone = exp(1j*2*pi*cfo*n/fs) as core.apply_cfo evaluates it (n = absolute index)
+            const double ph = w0 * (double)i / a.fs;
+            double sn, cs;
+            sincos(ph, &sn, &cs);
+            const double2 tone = make_double2(cs, sn);
+            for (int br = 0; br < a.nb; ++br) {
+                const double2 v = cmul(ld<FMT>(a.x, (b * a.nb + br) * a.T + i), tone);
+                acc.x += v.x; acc.y += v.y;
+            }
+            acc.x /= (double)a.nb; acc.y /= (double)a.nb;              // np.mean over branches
+        }
+        buf[bitrev(n, LB)] = acc;
+    }
+    __syncthreads();
+}
+
+template <int FMT>
+__global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double2 bsm[];
+    __shared__ double red[BW / 64];
+    __shared__ double scan_tot[BW / 64];
+    double2* buf = bsm;                       // N
+    double2* tw = bsm + a.N;                  // N / 2
+    double2* hs = tw + a.N / 2;               // n_used: h, later xhat
+    double* ph = reinterpret_cast<double*>(hs + a.n_used);   // n_used: phase / unwrap
+    const int64_t b = blockIdx.x;
+    const int N = a.N, U = a.n_used, LB = 31 - __clz(N);
+    for (int j = threadIdx.x; j < N / 2; j += BW) {
+        double sn, cs;
+        sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
+        tw[j] = make_double2(cs, sn);
+    }
+    // ---- CFO (core.py:179-196) or given ----
+    const int64_t ps = a.pilot_start[b];
+    double cfo;
+    if (a.cfo_in) {
+        cfo = a.cfo_in[b];
+    } else {
+        double pr = 0.0, pi = 0.0;
+        for (int idx = threadIdx.x; idx < a.nb * a.cp; idx += BW) {
+            const int br = idx / a.cp, n = idx - br * a.cp;
+            const int64_t i0 = ps + n, i1 = ps + a.N + n;
+            if (i0 >= 0 && i1 < a.T) {
+                const double2 u = ld<FMT>(a.x, (b * a.nb + br) * a.T + i0);
+                const double2 v = ld<FMT>(a.x, (b * a.nb + br) * a.T + i1);
+                pr += u.x * v.x + u.y * v.y;
+                pi += u.y * v.x - u.x * v.y;
+            }
+        }
+        pr = block_sum(pr, red);
+        pi = block_sum(pi, red);
+        cfo = -atan2(pi, pr) * a.fs / (2.0 * M_PI * (double)a.N);
+    }
+    if (a.cfo_out && threadIdx.x == 0) a.cfo_out[b] = cfo;
+    const double2* pil = a.pilot + b * a.pilot_stride;
+    const double2* dat = a.data + b * a.data_stride;
+    // ---- pilot: FFT, used bins, LS estimate ----
+    load_window<FMT>(a, b, ps + a.cp, cfo, buf, LB);
+    fft_lds(buf, tw, N, LB);
+    for (int u = threadIdx.x; u < U; u += BW) {
+        int k = a.bins[u] % N;
+        if (k < 0) k += N;
+        const double2 p = pil[u];
+        const double2 h = cdiv(buf[k], make_double2(p.x + 1e-9, p.y));      // y / (x + eps)
+        hs[u] = h;
+        ph[u] = atan2(h.y, h.x);
+        if (a.h_out) a.h_out[b * U + u] = h;
+    }
+    __syncthreads();
+    // ---- phase slope (core.py:443-469): unwrap = p + cumsum(correction), then the LS fit ----
+    {
+        // each thread owns a contiguous run of bins; correction[u] applies to bins >= u
+        const int per = (U + BW - 1) / BW;
+        const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
+        double local = 0.0;
+        for (int u = max(u0, 1); u < u1; ++u) {
+            const double dd = ph[u] - ph[u - 1];
+            double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+            if (dm == -M_PI && dd > 0.0) dm = M_PI;
+            local += fabs(dd) < M_PI ? 0.0 : dm - dd;
+        }
+        // exclusive block scan of the per-thread totals
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        double incl = local;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) scan_tot[w] = incl;
+        __syncthreads();
+        double base = incl - local;
+        for (int k = 0; k < w; ++k) base += scan_tot[k];
+        __syncthreads();
+        // rewrite ph[u] = unwrapped phase (reads of ph[u-1] done above, before the barrier)
+        double run = base, prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
+        __syncthreads();
+        for (int u = u0; u < u1; ++u) {
+            const double raw = ph[u];
+            if (u >= 1) {
+                const double dd = raw - prev_raw;
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                run += fabs(dd) < M_PI ? 0.0 : dm - dd;
+            }
+            prev_raw = raw;
+            ph[u] = raw + run;
+        }
+        __syncthreads();
+    }
+    double sk = 0.0, sp = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) { sk += (double)a.bins[u]; sp += ph[u]; }
+    const double kmean = block_sum(sk, red) / (double)U;
+    const double pmean = block_sum(sp, red) / (double)U;
+    double skk = 0.0, skp = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) {
+        const double kz = (double)a.bins[u] - kmean, pz = ph[u] - pmean;
+        skk += kz * kz; skp += kz * pz;
+    }
+    const double den = block_sum(skk, red) + 1e-12;
+    const double slope = block_sum(skp, red) / den;
+    if (threadIdx.x == 0) {
+        if (a.slope_out) a.slope_out[b] = slope;
+        if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
+    }
+    // ---- data: FFT, equalise, complex-gain alignment, EVM ----
+    load_window<FMT>(a, b, a.data_start[b] + a.cp, cfo, buf, LB);
+    fft_lds(buf, tw, N, LB);
+    double gr = 0.0, gi = 0.0, gx = 0.0, rr = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) {
+        int k = a.bins[u] % N;
+        if (k < 0) k += N;
+        const double2 h = hs[u];
+        const double2 xh = cdiv(buf[k], make_double2(h.x + 1e-9, h.y));    // equalize
+        hs[u] = xh;
+        const double2 r = dat[u];
+        gr += xh.x * r.x + xh.y * r.y;                                      // vdot(xhat, ref)
+        gi += xh.x * r.y - xh.y * r.x;
+        gx += xh.x * xh.x + xh.y * xh.y;                                    // vdot(xhat, xhat)
+        rr += r.x * r.x + r.y * r.y;
+    }
+    gr = block_sum(gr, red); gi = block_sum(gi, red); gx = block_sum(gx, red); rr = block_sum(rr, red);
+    const double2 g = cdiv(make_double2(gr, gi), make_double2(gx + 1e-12, 0.0));
+    double ee = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) {
+        const double2 xa = cmul(hs[u], g);
+        if (a.xa_out) a.xa_out[b * U + u] = xa;
+        const double2 r = dat[u];
+        const double er = xa.x - r.x, ei = xa.y - r.y;
+        ee += er * er + ei * ei;
+    }
+    ee = block_sum(ee, red);
+    if (threadIdx.x == 0) {
+        const double evm = sqrt((ee / (double)U) / (rr / (double)U));
+        if (a.gain_out) a.gain_out[b] = g;
+        if (a.evm_out) a.evm_out[b] = evm;
+        if (a.evm_db_out) a.evm_db_out[b] = 20.0 * log10(evm + 1e-12);
+    }
+}
+
+}  // namespace
+
+extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                                  int32_t n_fft, int32_t cp_len, double fs_hz, const int64_t* pilot_start,
+                                  const int64_t* data_start, const double* cfo_in, int32_t n_used,
+                                  const int32_t* bins, const void* pilot_used, int64_t pilot_stride,
+                                  const void* data_used, int64_t data_stride, double* cfo_out, void* h_out,
+                                  void* xa_out, void* gain_out, double* evm_out, double* evm_db_out,
+                                  double* slope_out, double* sto_out, void* stream) {
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || !x || B < 0 || n_br < 1 ||
+        T < 0 || n_fft < 2 || n_fft > BNMAX || (n_fft & (n_fft - 1)) || cp_len < 0 || n_used < 1 ||
+        n_used > n_fft || !pilot_start || !data_start || !bins || !pilot_used || !data_used ||
+        pilot_stride < 0 || data_stride < 0 || B > 0x7fffffff)
+        return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    BeArgs a{in_fmt, x, T, n_br, n_fft, cp_len, n_used, fs_hz, pilot_start, data_start, cfo_in, bins,
+             static_cast<const double2*>(pilot_used), pilot_stride, static_cast<const double2*>(data_used),
+             data_stride, cfo_out, static_cast<double2*>(h_out), static_cast<double2*>(xa_out),
+             static_cast<double2*>(gain_out), evm_out, evm_db_out, slope_out, sto_out};
+    const size_t lds = (size_t)n_fft * 16 + (size_t)(n_fft / 2) * 16 + (size_t)n_used * 24;
+    hipStream_t st = (hipStream_t)stream;
+    auto launch = [&](auto kern) -> int32_t {
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return OFS_EHIP;
+        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(BW), lds, st, a);
+        return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+    };
+    switch (in_fmt) {
+        case OFS_C64: return launch(rx_backend_kernel<OFS_C64>);
+        case OFS_C128: return launch(rx_backend_kernel<OFS_C128>);
+        default: return launch(rx_backend_kernel<OFS_CI16>);
+    }
+}

@@ -1,9 +1,10 @@
 """Drop-in for the CP-correlation CFO estimators of ``core.py`` (reference: core.py:179-336):
 estimate_cfo_from_cp, estimate_cfo_from_cp_robust, estimate_cfo_from_cp_peak[_with_index],
-find_cp_start_via_corr.
+find_cp_start_via_corr; plus the receiver back-end chain that sc.run_simulation runs after sync
+(sc.py:274-311: CFO removal, pilot FFT, LS channel estimate, phase-slope timing, equalisation,
+gain alignment, EVM) as one batched kernel (receiver_backend[_batched]).
 
-Only these hot-path functions are mirrored; the builders, plotting and receiver back-end of the
-reference's core.py are out of scope.
+The builders and plotting of the reference's core.py are out of scope.
 """
 from __future__ import annotations
 
@@ -135,3 +136,79 @@ def find_cp_start_via_corr(rx, est_start: int, n_fft: int, cp_len: int, search_h
         raise ValueError("cp_len must be positive")
     _, d, _, _ = _search_one(rx, est_start, n_fft, cp_len, max(0, int(search_half)), CPS_PEAK, 0.0)
     return d
+
+
+# ---------------------------------------------------------------------------------------------
+# receiver back-end after sync (the inline chain of sc.run_simulation, sc.py:274-311) ->
+# ofs_rx_backend
+# ---------------------------------------------------------------------------------------------
+def centered_subcarrier_indices(width: int) -> np.ndarray:
+    """Subcarrier indices symmetric around DC, skipping 0 (core.py:13-18)."""
+    half = width // 2
+    return np.concatenate((np.arange(-half, 0), np.arange(1, half + 1)))
+
+
+def receiver_backend_batched(x, pilot_start, data_start, pilot_used, data_used, *, n_fft: int = N_FFT,
+                             cp_len: int = CYCLIC_PREFIX, fs_hz: float = SAMPLE_RATE_HZ, bins=None,
+                             cfo_hz=None) -> dict:
+    """Per frame of x[B, n_branch, T]: CP CFO estimate at the pilot (unless cfo_hz [B] is given),
+    CFO removal + branch mean, pilot FFT -> LS channel estimate -> phase-slope timing, data
+    FFT -> equalise -> complex-gain alignment -> EVM.  pilot_used / data_used: [n_used] (shared)
+    or [B, n_used] known symbols.  Returns device tensors: cfo [B], h [B, n_used], xa [B, n_used],
+    gain [B] complex, evm, evm_db, slope, sto [B]."""
+    batch = _lib.as_batch(x, batched=True)
+    dev = batch.data.device
+    k = centered_subcarrier_indices(NUM_ACTIVE_SUBCARRIERS) if bins is None else np.asarray(bins)
+    U = int(k.size)
+
+    def dev_i64(v):
+        t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+        t = t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        if t.numel() == 1 and batch.B > 1:
+            t = t.expand(batch.B).contiguous()
+        if t.numel() != batch.B:
+            raise ValueError("one start per frame expected")
+        return t
+
+    def dev_ref(v):
+        t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v, dtype=np.complex128))
+        t = t.to(device=dev, dtype=torch.complex128).contiguous()
+        if t.shape[-1] != U or t.dim() > 2 or (t.dim() == 2 and t.shape[0] != batch.B):
+            raise ValueError("known symbols must be [n_used] or [B, n_used]")
+        return t, (U if t.dim() == 2 else 0)
+
+    ps, ds = dev_i64(pilot_start), dev_i64(data_start)
+    pil, pst = dev_ref(pilot_used)
+    dat, dst = dev_ref(data_used)
+    kb = torch.as_tensor(k.astype(np.int32)).to(dev)
+    cin = None if cfo_hz is None else torch.as_tensor(np.asarray(cfo_hz, np.float64)).to(dev).reshape(-1).contiguous()
+    B = batch.B
+    f64 = lambda: torch.empty((B,), dtype=torch.float64, device=dev)   # noqa: E731
+    out = dict(cfo=f64(), h=torch.empty((B, U), dtype=torch.complex128, device=dev),
+               xa=torch.empty((B, U), dtype=torch.complex128, device=dev),
+               gain=torch.empty((B,), dtype=torch.complex128, device=dev), evm=f64(), evm_db=f64(), slope=f64(),
+               sto=f64())
+    rc = _lib.lib().ofs_rx_backend(batch.fmt, batch.data.data_ptr(), B, batch.nb, batch.T, int(n_fft), int(cp_len),
+                                   float(fs_hz), ps.data_ptr(), ds.data_ptr(), _lib.ptr(cin), U, kb.data_ptr(),
+                                   pil.data_ptr(), pst, dat.data_ptr(), dst, out["cfo"].data_ptr(),
+                                   out["h"].data_ptr(), out["xa"].data_ptr(), out["gain"].data_ptr(),
+                                   out["evm"].data_ptr(), out["evm_db"].data_ptr(), out["slope"].data_ptr(),
+                                   out["sto"].data_ptr(), _lib.stream_ptr())
+    _lib.check(rc, "ofs_rx_backend")
+    return out
+
+
+def receiver_backend(rx, pilot_cp_start: int, data_cp_start: int, pilot_used, data_used, *, cfo_hz=None,
+                     n_fft: int = N_FFT, cp_len: int = CYCLIC_PREFIX, fs_hz: float = SAMPLE_RATE_HZ) -> dict:
+    """One frame (1-D or [branches, T]) through the back-end chain of sc.run_simulation
+    (sc.py:274-311); numpy / Python scalars out, keys as receiver_backend_batched."""
+    a = rx if isinstance(rx, torch.Tensor) else np.asarray(rx)
+    x = a[None] if a.ndim == 1 else a
+    out = receiver_backend_batched(x[None], [pilot_cp_start], [data_cp_start], pilot_used, data_used,
+                                   n_fft=n_fft, cp_len=cp_len, fs_hz=fs_hz,
+                                   cfo_hz=None if cfo_hz is None else [cfo_hz])
+    res = {}
+    for key, v in out.items():
+        v = v[0].cpu()
+        res[key] = v.numpy() if v.dim() else (complex(v.item()) if v.is_complex() else float(v.item()))
+    return res

@@ -24,6 +24,7 @@ __all__ = [
     "aa_metric", "aa_events", "aa_detect",
     "sc_metric", "comb_sc_metric", "minn_metric",
     "minn_rtl_metric", "detect_minn_rtl", "cp_cfo", "cp_cfo_robust", "cp_cfo_peak", "find_cp_start",
+    "rx_backend",
     "park_metric", "zc_template", "zc_freq_metric", "pss_symbol", "matched_filter",
     "normalize_correlation", "zc_combined", "zc_streaming_detection", "detect_zc_peaks",
     "trailing_average", "plateau_end", "minn_peak", "sc_gate", "streaming_peak", "comb_minn_peak",
@@ -362,6 +363,41 @@ def find_cp_start(rx, est, n_fft, cp_len, search_half=1024):
         if v > bv:
             bv, bd = v, d
     return int(bd)
+
+
+# ---------------------------------------------------------------------------------------
+# receiver back-end chain of sc.run_simulation (sc.py:274-311) over core.py helpers
+# ---------------------------------------------------------------------------------------
+def rx_backend(rx, pilot_start, data_start, n_fft, cp, fs, bins, pilot_used, data_used, cfo=None):
+    """cfo = estimate_cfo_from_cp at the pilot CP (core.py:179-196) unless given; rx_eff =
+    branch mean of apply_cfo(rx, -cfo) (core.py:123-138); y = fftshift(fft(window))[(N/2+k)%N]
+    (ofdm_fft_used, core.py:171-176); h = y_p/(pilot+1e-9) (:339-341); slope/sto from the
+    unwrapped phase of h (:443-469, abscissa = bins); xhat = y_d/(h+1e-9) (:344-345);
+    gain = vdot(xhat, ref)/(vdot(xhat, xhat)+1e-12) (:357-362); evm (:365-370)."""
+    x = _as2d(rx)
+    if cfo is None:
+        cfo = cp_cfo(x, pilot_start, n_fft, cp, fs)[0]
+    n = np.arange(x.shape[1], dtype=float)
+    tone = np.exp(1j * 2 * np.pi * (-cfo) * n / fs)
+    eff = np.mean(x * tone[np.newaxis, :], axis=0)
+    k = np.asarray(bins)
+
+    def used(s):
+        spec = np.fft.fftshift(np.fft.fft(eff[s + cp:s + cp + n_fft], n=n_fft))
+        return spec[(n_fft // 2 + k) % n_fft]
+
+    h = used(pilot_start) / (np.asarray(pilot_used) + 1e-9)
+    phi = np.unwrap(np.angle(h))
+    kz = k.astype(float) - np.mean(k.astype(float))
+    pz = phi - np.mean(phi)
+    slope = float(np.sum(kz * pz) / (float(np.sum(kz * kz)) + 1e-12))
+    xhat = used(data_start) / (h + 1e-9)
+    ref = np.asarray(data_used)
+    g = np.vdot(xhat, ref) / (np.vdot(xhat, xhat) + 1e-12)
+    xa = xhat * g
+    evm = float(np.sqrt(np.mean(np.abs(xa - ref) ** 2) / np.mean(np.abs(ref) ** 2)))
+    return dict(cfo=float(cfo), h=h, xa=xa, gain=complex(g), evm=evm, evm_db=float(20 * np.log10(evm + 1e-12)),
+                slope=slope, sto=float(-slope * n_fft / (2 * np.pi)))
 
 
 # ---------------------------------------------------------------------------------------

@@ -263,6 +263,42 @@ def gen_cp_cfo(R, cases):
     cases["cp_search"] = srch
 
 
+def gen_backend(R, cases):
+    """Receiver back-end chain of sc.run_simulation (sc.py:274-311), run with the reference's
+    own core.py helpers on frames built by its builders; the pilot/data CP starts are the true
+    ones shifted by a few samples (the detector's job is upstream)."""
+    core, ch = R["core"], R["channel"]
+    N, CP, fs = core.N_FFT, core.CYCLIC_PREFIX, core.SAMPLE_RATE_HZ
+    k = core.centered_subcarrier_indices(core.NUM_ACTIVE_SUBCARRIERS)
+    for name, seed, snr, cir, cfo, shift in (("backend_cir1_2br", 21, 15.0, "cir1", 1000.0, 3),
+                                             ("backend_awgn_1br", 22, 20.0, None, -2500.0, 0),
+                                             ("backend_cir2_2br_early", 23, 10.0, "cir2", 700.0, -4)):
+        rng = np.random.default_rng(seed)
+        pil, pil_used = core.build_random_qpsk_symbol(rng, include_cp=True)
+        dat, dat_used = core.build_random_qpsk_symbol(rng, include_cp=True)
+        pad = 600
+        tx = np.concatenate([np.zeros(pad, complex), pil, dat, np.zeros(300, complex)])
+        rx = ch.apply_channel(tx, snr, rng, None if cir is None else ch.load_measured_cir(cir)[:2])
+        rx = core.apply_cfo(rx, cfo, fs)
+        ps = pad + shift
+        ds = ps + CP + N
+        cfo_est = core.estimate_cfo_from_cp(rx, ps, N, CP, fs)        # sc.py:278-284
+        rxc = core.apply_cfo(rx, -cfo_est, fs)                         # sc.py:286
+        eff = rxc if rxc.ndim == 1 else np.mean(rxc, axis=0)           # sc.py:289
+        y_p = core.ofdm_fft_used(eff[ps + CP:ps + CP + N])
+        h = core.ls_channel_estimate(y_p, pil_used)
+        slope, sto = core.estimate_timing_offset_from_phase_slope(h)
+        y_d = core.ofdm_fft_used(eff[ds + CP:ds + CP + N])
+        xhat = core.equalize(y_d, h)
+        xa, gain = core.align_complex_gain(xhat, dat_used)
+        evm, evm_db = core.evm_rms_db(xa, dat_used)
+        cases[name] = dict(kind="backend", x=np.atleast_2d(rx), pilot_start=np.int64(ps), data_start=np.int64(ds),
+                           n_fft=np.int64(N), cp=np.int64(CP), fs=np.float64(fs), bins=k.astype(np.int64),
+                           pilot_used=pil_used, data_used=dat_used, cfo=np.float64(cfo_est), h=h, xa=xa,
+                           gain=np.complex128(gain), evm=np.float64(evm), evm_db=np.float64(evm_db),
+                           slope=np.float64(slope), sto=np.float64(sto), y_pilot=y_p)
+
+
 def gen_park(R, cases):
     pk = R["park"]
     core = R["core"]
@@ -431,6 +467,7 @@ def main():
     gen_combined(R, cases)
     gen_minn_rtl(R, cases)
     gen_cp_cfo(R, cases)
+    gen_backend(R, cases)
     gen_park(R, cases)
     gen_zc(R, cases)
     gen_post(R, cases)

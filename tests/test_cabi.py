@@ -78,6 +78,11 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ofs_cp_search(0, 1, 1, 1, 16, 1, 8, 0, 2, 0, 1.0, None, None, 1, 1, None) == -1
     assert lib.ofs_cp_search(0, 1, 1, 1, 16, 1, 8, 4, 2, 5, 1.0, None, None, 1, 1, None) == -1
     assert lib.ofs_minn_rtl_gate(None, None, None, 1, 16, 2, 0, 1, None, None, None, None) == -1
+    # receiver back-end: N not a power of two, n_used > N, missing starts
+    bk = (0, 1, 1, 1, 64)
+    assert lib.ofs_rx_backend(*bk, 48, 8, 1.0, 1, 1, None, 8, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
+    assert lib.ofs_rx_backend(*bk, 32, 8, 1.0, 1, 1, None, 40, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
+    assert lib.ofs_rx_backend(*bk, 32, 8, 1.0, None, 1, None, 8, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
     # empty batches are valid no-ops
     assert lib.ofs_sc_metric(0, 1, 0, 1, 16, 8, 0, 0, None, None, None, None) == 0
     assert lib.ofs_minn_metric(0, 1, 1, 1, 4, 8, 0, None, None, None, None) == 0

@@ -463,3 +463,56 @@ def test_aa_fast_path_sweep(L, T):
 def test_aa_fast_path_is_used_for_the_benchmark_shape():
     assert _lib.lib().ofs_aa_plan(_lib.C64, _lib.FP32, 1, 1024, 512) >= 1000
     assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, 1, 1024, 512) in (1, 2)
+
+
+# ------------------------------------------------------ receiver back-end ------------
+@pytest.mark.parametrize("name", cases("backend"))
+def test_receiver_backend_vs_reference_golden(name):
+    """sc.run_simulation's back-end chain (sc.py:274-311) on reference-built frames: CFO,
+    channel estimate, aligned constellation and EVM within 1e-9 relative; STO / slope 1e-9."""
+    d = G(name)
+    kw = dict(n_fft=int(d["n_fft"]), cp_len=int(d["cp"]), fs_hz=float(d["fs"]))
+    r = core.receiver_backend(d["x"], int(d["pilot_start"]), int(d["data_start"]), d["pilot_used"],
+                              d["data_used"], **kw)
+    assert abs(r["cfo"] - float(d["cfo"])) < 1e-7
+    assert relerr(r["h"], d["h"]) < 1e-9
+    assert relerr(r["xa"], d["xa"]) < 1e-9
+    assert abs(r["gain"] - complex(d["gain"])) < 1e-9 * max(1.0, abs(complex(d["gain"])))
+    assert abs(r["evm"] - float(d["evm"])) < 1e-9 * max(1.0, float(d["evm"]))
+    assert abs(r["evm_db"] - float(d["evm_db"])) < 1e-7
+    assert abs(r["slope"] - float(d["slope"])) < 1e-9
+    assert abs(r["sto"] - float(d["sto"])) < 1e-6
+    # given-CFO path and a batch (one frame per row, per-frame known symbols)
+    rg = core.receiver_backend(d["x"], int(d["pilot_start"]), int(d["data_start"]), d["pilot_used"],
+                               d["data_used"], cfo_hz=float(d["cfo"]), **kw)
+    assert relerr(rg["h"], d["h"]) < 1e-9
+    xb = torch.from_numpy(np.stack([d["x"]] * 3)).cuda()
+    out = core.receiver_backend_batched(xb, [int(d["pilot_start"])] * 3, [int(d["data_start"])] * 3,
+                                        np.stack([d["pilot_used"]] * 3), d["data_used"], **kw)
+    assert relerr(out["xa"].cpu().numpy()[2], d["xa"]) < 1e-9
+    assert np.allclose(out["evm"].cpu().numpy(), float(d["evm"]), rtol=1e-9)
+
+
+@pytest.mark.parametrize("fmt,nb,N", [("c64", 1, 2048), ("int16", 2, 1024), ("c128", 3, 256)])
+def test_receiver_backend_batched_vs_oracle(fmt, nb, N):
+    rng = np.random.default_rng(N + nb)
+    B, cp = 6, N // 4
+    k = core.centered_subcarrier_indices(N // 2)
+    T = 2 * (N + cp) + 400
+    x = (rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))) * 300
+    x = np.round(x)
+    ps = rng.integers(0, 100, B)
+    ds = ps + N + cp
+    pil = np.exp(2j * np.pi * rng.random((B, k.size)))
+    dat = np.exp(2j * np.pi * rng.random(k.size))
+    if fmt == "int16":
+        xd = torch.from_numpy(np.stack([x.real, x.imag], -1).astype(np.int16)).cuda()
+    else:
+        xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
+    out = core.receiver_backend_batched(xd, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
+    for b in range(B):
+        r = O.rx_backend(x[b], int(ps[b]), int(ds[b]), N, cp, 1e6, k, pil[b], dat)
+        assert abs(out["cfo"][b].item() - r["cfo"]) < 1e-6
+        assert relerr(out["h"][b].cpu().numpy(), r["h"]) < 1e-9
+        assert relerr(out["xa"][b].cpu().numpy(), r["xa"]) < 1e-8
+        assert abs(out["evm"][b].item() - r["evm"]) < 1e-8 * max(1.0, r["evm"])

@@ -71,6 +71,15 @@ def test_oracle_matches_reference_golden(path):
         assert np.allclose(c, d["cfo"], rtol=0, atol=1e-9)
         c1 = [O.cp_cfo(d["x"][0], int(s), 2048, 256, float(d["fs_1br"]))[0] for s in d["starts"]]
         assert np.allclose(c1, d["cfo_1br_cp256"], rtol=0, atol=1e-9)
+    elif kind == "backend":
+        r = O.rx_backend(d["x"], int(d["pilot_start"]), int(d["data_start"]), int(d["n_fft"]), int(d["cp"]),
+                         float(d["fs"]), d["bins"], d["pilot_used"], d["data_used"])
+        assert abs(r["cfo"] - float(d["cfo"])) < 1e-9
+        for k in ("h", "xa"):
+            assert np.allclose(r[k], d[k], rtol=1e-12, atol=1e-12), k
+        for k in ("evm", "evm_db", "slope", "sto"):
+            assert abs(r[k] - float(d[k])) < 1e-9, k
+        assert abs(r["gain"] - complex(d["gain"])) < 1e-12
     elif kind == "cp_search":
         x, N, cp, fs = d["x"], int(d["n_fft"]), int(d["cp_len"]), float(d["fs"])
         est = [int(e) for e in d["est"]]

@@ -159,7 +159,37 @@ def cfg5(dev, st, steps, warmup, n_seq=1 << 20):
                 bytes_per_sample="8 in + 4|8 B per sequence out")
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5}
+def backend(dev, st, steps, warmup):
+    """Receiver back-end (sc.py:274-311 chain) over a batch of frames: 2 branches, N = 2048,
+    CP = 512, c64 input; CP CFO, two 2048-point FFTs, LS, phase-slope STO, EQ, EVM per frame."""
+    from ofdm_sync_amd import core
+    B, nb, N, cp = 16384, 2, 2048, 512
+    T = 2 * (N + cp) + 64
+    g = torch.Generator(device=dev).manual_seed(11)
+    x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    k = core.centered_subcarrier_indices(1200)
+    U = k.size
+    ps = torch.full((B,), 32, dtype=torch.int64, device=dev)
+    ds = ps + N + cp
+    pil = torch.ones((U,), dtype=torch.complex128, device=dev)
+    kb = torch.as_tensor(k.astype(np.int32)).to(dev)
+    outs = [torch.empty((B,), dtype=torch.float64, device=dev) for _ in range(5)]
+    h = torch.empty((B, U), dtype=torch.complex128, device=dev)
+    xa = torch.empty_like(h)
+    gain = torch.empty((B,), dtype=torch.complex128, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), B, nb, T, N, cp, 30.72e6, ps.data_ptr(), ds.data_ptr(), None, U, kb.data_ptr(),
+            pil.data_ptr(), 0, pil.data_ptr(), 0, outs[0].data_ptr(), h.data_ptr(), xa.data_ptr(), gain.data_ptr(),
+            outs[1].data_ptr(), outs[2].data_ptr(), outs[3].data_ptr(), outs[4].data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_rx_backend(*args), "rx_backend"), steps, warmup, st)
+    nbytes = B * (nb * (2 * N + 2 * cp) * 8 + 2 * U * 16 + 5 * 8 + 16)
+    return dict(config="backend", workload=f"receiver back-end, {B} frames x {nb} branches, N={N}, CP={cp}, c64 in, fp64",
+                kernel="rx_backend_kernel (LDS radix-2 FFTs, one workgroup per frame)", samples=B * nb * 2 * N,
+                ms=ms, alg_bytes=nbytes, bytes_per_sample="windows read once (8 B) + 2 x 16 B per used bin out",
+                frames_per_s=round(B / (ms / 1e3), 1))
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
 
 
 def main():
