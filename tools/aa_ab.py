@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--L", type=int, default=512)
     ap.add_argument("--realloc", type=int, default=0, help="only the full case, re-allocating all buffers N times")
     ap.add_argument("--same", action="store_true", help="realloc sweep without re-allocating (time variation)")
+    ap.add_argument("--pre", type=float, default=0.0, help="GiB allocated (and held) before the first round")
     ap.add_argument("--libs", default="", help="comma list of library paths timed on the same buffers (realloc)")
     a = ap.parse_args()
     if a.realloc:
@@ -79,6 +80,7 @@ def realloc_sweep(a):
         libs.append((os.path.basename(path), l))
     st = torch.cuda.current_stream(dev)
     keep = []
+    pre = torch.empty(int(a.pre * (1 << 30)), dtype=torch.uint8, device=dev) if a.pre > 0 else None
     for r in range(a.realloc):
         if a.same and keep:
             x, P, R, M = keep[0]
