@@ -170,8 +170,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 (c64 in, f64 prefix sums)",
-            "data": "synthetic: [A][A] ZC preamble (sync_aa.build_aa_preamble restated) * cir1 ch1 "
-                    "+ AWGN U[0,15] dB + CFO U[-5,5] kHz @ 15.36 MHz, random window offset",
+            "data": "synthetic (ofs_synth_batch on the GPU): [A][A] ZC preamble (sync_aa.build_aa_preamble "
+                    "restated) * cir1 ch1 + AWGN U[0,15] dB + CFO U[-5,5] kHz @ 15.36 MHz, random window offset",
             "config": {"workload": "cfg3 Schmidl-Cox float32 metric+CFO, N=1024 (L=512), cir1, "
                                    f"{B} streams x {T} c64 per GPU",
                        "global_batch": world * B, "seq_len": T, "L": L,

@@ -213,6 +213,22 @@ int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, i
                        double* slope_out, double* sto_out, void* stream);
 
 /*
+ * Batched receive-stream synthesis (benchmark / test input): the channel +
+ * impairment chain of channel.apply_channel (channel.py:80-98), core.apply_cfo
+ * (core.py:123-138) and sync_aa.quantize_adc (sync_aa.py:263-291):
+ *   out[b][br][n] = q(base[br][off_b + n] * exp(i 2 pi cfo_b n / fs) + CN(0, 10^(-snr_b/10)))
+ * with off_b ~ U{0..max_offset-1}, snr_b ~ U[snr_lo, snr_hi] dB, cfo_b ~ U[cfo_lo, cfo_hi] Hz drawn
+ * per stream from Philox-4x32-10(seed, b) (distribution-level, not numpy's stream).
+ *   base: [n_br][base_len] c128 (device; unit-power faded preamble, zero past its end);
+ *   out_fmt OFS_C64 | OFS_C128 | OFS_CI16 (q = round(x * adc_scale) clipped to [-2048, 2047]);
+ *   out: [B][n_br][T]; params: [B][3] f64 = offset, snr_db, cfo_hz (nullable).
+ */
+int32_t ofs_synth_batch(const void* base, int64_t base_len, int32_t n_br, int64_t B, int64_t T,
+                        int32_t max_offset, double snr_lo_db, double snr_hi_db, double cfo_lo_hz,
+                        double cfo_hi_hz, double fs_hz, uint64_t seed, int32_t out_fmt,
+                        double adc_scale, void* out, double* params, void* stream);
+
+/*
  * Park mirror-symmetry metric: replaces park.park_streaming_metric (park.py:64-114).
  * half = N/2; outputs for d in [half, T-half-1], n_out = T - 2*half, laid out [B][n_out]:
  *   P (c64|c128) = sum_br sum_{k<half} x[d-k]*x[d+k]; E (f32|f64) = sum_br sum_{k<half}|x[d+k]|^2;

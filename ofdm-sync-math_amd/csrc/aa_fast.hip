@@ -271,7 +271,7 @@ int pick_e(int L) {
         forced = s ? atoi(s) : 0;
     }
     if (forced == 2 || forced == 4 || forced == 8) return (L % (64 * forced) == 0) ? forced : 0;
-    for (int e : {4, 2, 8})
+    for (int e : {2, 4, 8})                                  // E=2 measured 3 % faster than 4 (r01c)
         if (L % (64 * e) == 0) return e;
     return 0;
 }

@@ -4,8 +4,8 @@ Restates the reference's input builders closely enough to produce realistic stre
   aa_preamble      <- sync_aa.build_aa_preamble (sync_aa.py:160-235)
   load_cir         <- channel.load_measured_cir (channel.py:15-48)
   make_aa_batch    <- run_single_test's channel + AWGN + CFO chain (sync_aa.py:577-645),
-                      vectorised over a batch on the GPU (torch ops; RNG parity with numpy is
-                      not a goal, only the distribution: SURVEY.md §8f row 2).
+  synth_batch         generated per stream on the GPU by ofs_synth_batch (csrc/synth.hip;
+                      Philox RNG: distribution-level parity with numpy).
 """
 from __future__ import annotations
 
@@ -13,6 +13,8 @@ import os
 
 import numpy as np
 import torch
+
+from . import _lib
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 CIR_DIR = os.path.join(_HERE, "channel_models")
@@ -51,10 +53,67 @@ def load_cir(name: str = "cir1") -> np.ndarray:
     return out
 
 
+def faded_base(L: int = 512, cir: str | None = "cir1", branches=(1,)) -> np.ndarray:
+    """[n_branch, len] unit-power faded [A][A] preamble (preamble ⊛ CIR of each branch), the
+    deterministic part of every synthesised stream."""
+    pre = aa_preamble(2 * L)
+    rows = []
+    for br in branches:
+        y0 = pre if cir is None else np.convolve(pre, load_cir(cir)[br])
+        rows.append(y0 / np.sqrt(np.mean(np.abs(y0[: 2 * L]) ** 2)))
+    n = max(len(r) for r in rows)
+    out = np.zeros((len(rows), n), complex)
+    for i, r in enumerate(rows):
+        out[i, :len(r)] = r
+    return out
+
+
+_FMT = {torch.complex64: _lib.C64, torch.complex128: _lib.C128, torch.int16: _lib.CI16}
+
+
+def synth_batch(base, B: int, T: int, *, max_offset: int = 128, snr_db=(0.0, 15.0), cfo_hz=(-5000.0, 5000.0),
+                fs: float = 15.36e6, seed: int = 2026, device="cuda", dtype=torch.complex64,
+                adc_scale: float = 1024.0, return_params: bool = False):
+    """ofs_synth_batch: [B, n_branch, T] streams = base shifted by a random offset, CFO tone,
+    AWGN at a random SNR (per stream), optionally int12-quantised (dtype=torch.int16 -> I/Q
+    pairs in a trailing axis).  Generated on the GPU in one kernel."""
+    base = np.atleast_2d(np.asarray(base, np.complex128))
+    nb, Lb = base.shape
+    dev = torch.device(device)
+    bt = torch.from_numpy(np.ascontiguousarray(base)).to(dev)
+    if dtype not in _FMT:
+        raise TypeError(f"unsupported output dtype {dtype}")
+    shape = (B, nb, T, 2) if dtype == torch.int16 else (B, nb, T)
+    out = torch.empty(shape, dtype=dtype, device=dev)
+    params = torch.empty((B, 3), dtype=torch.float64, device=dev) if return_params else None
+    with torch.cuda.device(dev):
+        rc = _lib.lib().ofs_synth_batch(bt.data_ptr(), Lb, nb, B, T, int(max_offset), float(snr_db[0]),
+                                        float(snr_db[1]), float(cfo_hz[0]), float(cfo_hz[1]), float(fs),
+                                        int(seed) & ((1 << 64) - 1), _FMT[dtype], float(adc_scale), out.data_ptr(),
+                                        _lib.ptr(params), torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(rc, "ofs_synth_batch")
+    torch.cuda.current_stream(dev).synchronize()           # `bt` is freed on return
+    return (out, params) if return_params else out
+
+
 def make_aa_batch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, cir: str | None = "cir1",
                   branch: int = 1, snr_db=(0.0, 15.0), cfo_hz=(-5000.0, 5000.0), fs: float = 15.36e6,
                   max_offset: int = 128, device="cuda", dtype=torch.complex64) -> torch.Tensor:
     """Batch [B, 1, T] of received [A][A] preambles: CIR (one branch) + AWGN + CFO, unit power.
+
+    Each stream is a T-sample window of the faded preamble starting at a random offset in
+    [0, max_offset); SNR and CFO are drawn uniformly per stream (ofs_synth_batch on the GPU).
+    """
+    return synth_batch(faded_base(L, cir, (branch,)), B, T, max_offset=max_offset, snr_db=snr_db, cfo_hz=cfo_hz,
+                       fs=fs, seed=seed, device=device, dtype=dtype)
+
+
+def make_aa_batch_torch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, cir: str | None = "cir1",
+                        branch: int = 1, snr_db=(0.0, 15.0), cfo_hz=(-5000.0, 5000.0), fs: float = 15.36e6,
+                        max_offset: int = 128, device="cuda", dtype=torch.complex64) -> torch.Tensor:
+    """make_aa_batch with torch ops on any device (CPU included): the input generator of the
+    CPU-only multi-process tests (gloo), where the HIP kernel cannot run.  Same distribution,
+    different random stream.
 
     Each stream is a T-sample window of the faded preamble starting at a random offset in
     [0, max_offset); SNR and CFO are drawn uniformly per stream.

@@ -83,6 +83,10 @@ def test_argument_validation_without_gpu(lib):
     assert lib.ofs_rx_backend(*bk, 48, 8, 1.0, 1, 1, None, 8, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
     assert lib.ofs_rx_backend(*bk, 32, 8, 1.0, 1, 1, None, 40, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
     assert lib.ofs_rx_backend(*bk, 32, 8, 1.0, None, 1, None, 8, 1, 1, 0, 1, 0, *([None] * 8), None) == -1
+    # synthesis: null base, bad output format, non-positive sample rate
+    assert lib.ofs_synth_batch(None, 8, 1, 1, 8, 0, 0.0, 1.0, 0.0, 0.0, 1.0, 1, 0, 1.0, 1, None, None) == -1
+    assert lib.ofs_synth_batch(1, 8, 1, 1, 8, 0, 0.0, 1.0, 0.0, 0.0, 1.0, 1, 9, 1.0, 1, None, None) == -1
+    assert lib.ofs_synth_batch(1, 8, 1, 1, 8, 0, 0.0, 1.0, 0.0, 0.0, 0.0, 1, 0, 1.0, 1, None, None) == -1
     # empty batches are valid no-ops
     assert lib.ofs_sc_metric(0, 1, 0, 1, 16, 8, 0, 0, None, None, None, None) == 0
     assert lib.ofs_minn_metric(0, 1, 1, 1, 4, 8, 0, None, None, None, None) == 0

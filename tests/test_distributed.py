@@ -29,7 +29,7 @@ def _worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     d = shard.init("gloo")
-    x = synth.make_aa_batch(B_TOTAL, T, L, seed=5, device="cpu").numpy()
+    x = synth.make_aa_batch_torch(B_TOTAL, T, L, seed=5, device="cpu").numpy()
     lo, hi = shard.shard_bounds(B_TOTAL, rank, world)
     r = oracle_c.aa_detect(x[lo:hi], L, max_events=4, nthreads=1)
     counts = shard.gather_counts(torch.from_numpy(r["n_events"].astype(np.int64)), d)
@@ -58,7 +58,7 @@ def test_world2_gloo_matches_single_process(tmp_path):
     port = _free_port()
     mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     got = np.load(tmp_path / "dist.npz")
-    x = synth.make_aa_batch(B_TOTAL, T, L, seed=5, device="cpu").numpy()
+    x = synth.make_aa_batch_torch(B_TOTAL, T, L, seed=5, device="cpu").numpy()
     ref = oracle_c.aa_detect(x, L, max_events=4, nthreads=1)
     assert np.array_equal(got["counts"], ref["n_events"])
     assert np.array_equal(got["peaks"], ref["ev_int"][:, 0, 0])
