@@ -31,7 +31,7 @@ def alloc(flags):
     return rc, p.value
 
 
-def run(base, steps=60):
+def run(base, steps=int(os.environ.get("PROBE_STEPS", "60"))):
     hip.hipMemcpy(ctypes.c_void_p(base), ctypes.c_void_p(x0.data_ptr()), ctypes.c_size_t(NX), 3)
     args = (_lib.C64, base, B, 1, T, L, _lib.FP32, base + NX, base + 2 * NX, base + 2 * NX + NR, None, 1,
             0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
