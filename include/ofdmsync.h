@@ -72,7 +72,7 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
 /*
  * Which kernel ofs_aa_detect dispatches a shape to (pure query, no launch):
  *   1000 + 10*E + MR : register-resident wave-per-stream fast path (E samples per lane,
- *                      L = 64*E*MR), complex64 / OFS_FP32 / one antenna / even T <= 1024;
+ *                      L = 64*E*MR), complex64 / OFS_FP32 / 1-2 antennas / even T <= 1024;
  *   2000 + 10*E + MR : integer-exact wave-per-stream path, OFS_CI16 / OFS_FP64, 1-2 antennas,
  *                      T * n_ant <= 2^21 (all window sums exact integers), L = 64*E*MR, MR <= 8;
  *   1                : general LDS engine, events fused (stream fits one tile);

@@ -74,7 +74,7 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 // ds_read_b128.  Paired A/B on the same buffers: registers 1-3 % faster (profiles/
 // r01c_staging_ab.log; the SOL probe shows the same 8 % gap between LDS-DMA and register staging
 // of this read/write pattern).
-template <int E, int MR>
+template <int E, int MR, int NA>
 __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;                 // samples per row
     constexpr int RW = TMAX / RL;              // rows per stream
@@ -82,7 +82,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int V4 = E / 2;                  // float4 (2 samples) per lane per row
     static_assert(MR >= 1 && MR <= RW, "window must fit the stream tile");
 #if OFS_FAST_STAGE == 0
-    __shared__ float4 lds[FAST_WG / 64][RW * V4][64];
+    __shared__ float4 lds[FAST_WG / 64][NA * RW * V4][64];
 #endif
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -90,8 +90,9 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     if (b >= a.B) return;
     const int T = (int)a.T;
 #if OFS_FAST_STAGE == 0
-    {
-        const float2* xs = reinterpret_cast<const float2*>(a.x) + b * a.T;
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+        const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * NA + t) * a.T;
 #pragma unroll
         for (int k = 0; k < RW; ++k)
 #pragma unroll
@@ -99,33 +100,34 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                 int n = RL * k + E * lane + 2 * j;
                 n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
                 __builtin_amdgcn_global_load_lds((const void*)(xs + n),
-                                                 (__attribute__((address_space(3))) void*)&lds[w][k * V4 + j][0],
+                                                 (__attribute__((address_space(3))) void*)&lds[w][(t * RW + k) * V4 + j][0],
                                                  16, 0, OFS_DMA_AUX);
             }
     }
-    auto ldrow = [&](int k, int j) { return lds[w][k * V4 + j][lane]; };
+    auto ldrow = [&](int t, int k, int j) { return lds[w][(t * RW + k) * V4 + j][lane]; };
 #else
     // register staging: every row of the lane's samples is loaded up front (RW * V4 float4), each
     // row's first use waits only for its own loads (vmcnt counts in order)
-    float4 xreg[RW][V4];
-    {
-        const float2* xs = reinterpret_cast<const float2*>(a.x) + b * a.T;
+    float4 xreg[NA][RW][V4];
+#pragma unroll
+    for (int t = 0; t < NA; ++t) {
+        const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * NA + t) * a.T;
 #pragma unroll
         for (int k = 0; k < RW; ++k)
 #pragma unroll
             for (int j = 0; j < V4; ++j) {
                 int n = RL * k + E * lane + 2 * j;
                 n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
-                xreg[k][j] = *reinterpret_cast<const float4*>(xs + n);
+                xreg[t][k][j] = *reinterpret_cast<const float4*>(xs + n);
             }
     }
-    auto ldrow = [&](int k, int j) { return xreg[k][j]; };
+    auto ldrow = [&](int t, int k, int j) { return xreg[t][k][j]; };
 #endif
-    auto xrow = [&](int k, float (&re)[E], float (&im)[E]) {
+    auto xrow = [&](int t, int k, float (&re)[E], float (&im)[E]) {
 #pragma unroll
         for (int j = 0; j < V4; ++j) {
             const bool ok = RL * k + E * lane + 2 * j < T;
-            const float4 v = ldrow(k, j);
+            const float4 v = ldrow(t, k, j);
             re[2 * j] = ok ? v.x : 0.f; im[2 * j] = ok ? v.y : 0.f;
             re[2 * j + 1] = ok ? v.z : 0.f; im[2 * j + 1] = ok ? v.w : 0.f;
         }
@@ -150,23 +152,25 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
         if (RL * k < T) {                                       // wave-uniform row guard
             const int nb = RL * k + E * lane;                   // first sample of this lane
             // ---- lagged products x[n]·conj(x[n-L]) and energies, fp32 ----
+            // summed over the antennas, like the reference's per-antenna running sums added up
+            // (sync_aa.py:463-480)
             float aR[E], aI[E], aE[E];
-            {
-                float cr[E], ci[E];
-                xrow(k, cr, ci);
 #pragma unroll
-                for (int e = 0; e < E; ++e) aE[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
+            for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+#pragma unroll
+            for (int t = 0; t < NA; ++t) {
+                float cr[E], ci[E];
+                xrow(t, k, cr, ci);
+#pragma unroll
+                for (int e = 0; e < E; ++e) aE[e] += fmaf(cr[e], cr[e], ci[e] * ci[e]);
                 if (k >= MR) {
                     float dr[E], di[E];
-                    xrow(k - MR, dr, di);
+                    xrow(t, k - MR, dr, di);
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
-                        aR[e] = fmaf(cr[e], dr[e], ci[e] * di[e]);
-                        aI[e] = fmaf(ci[e], dr[e], -(cr[e] * di[e]));
+                        aR[e] += fmaf(cr[e], dr[e], ci[e] * di[e]);
+                        aI[e] += fmaf(ci[e], dr[e], -(cr[e] * di[e]));
                     }
-                } else {
-#pragma unroll
-                    for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; }
                 }
             }
             // ---- in-lane partials, each summing only the terms it stands for:
@@ -237,28 +241,29 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     if (a.detect) gate.finish(lane, T, a.n_ev + b);
 }
 
-template <int E, int MR>
+template <int E, int MR, int NA>
 int launch(const AaFastArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + 3) / 4;
-    hipLaunchKernelGGL((aa_fast_kernel<E, MR>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
+    hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
-template <int E, int MR = 1>
+template <int E, int NA, int MR = 1>
 int launch_mr(int mr, const AaFastArgs& a, hipStream_t st) {
     if constexpr (MR > TMAX / (64 * E)) {
         return 0;
     } else {
-        if (mr == MR) return launch<E, MR>(a, st);
-        return launch_mr<E, MR + 1>(mr, a, st);
+        if (mr == MR) return launch<E, MR, NA>(a, st);
+        return launch_mr<E, NA, MR + 1>(mr, a, st);
     }
 }
 
+template <int NA>
 int launch_e(int E, int mr, const AaFastArgs& a, hipStream_t st) {
     switch (E) {
-        case 2: return launch_mr<2>(mr, a, st);
-        case 4: return launch_mr<4>(mr, a, st);
-        case 8: return launch_mr<8>(mr, a, st);
+        case 2: return launch_mr<2, NA>(mr, a, st);
+        case 4: return launch_mr<4, NA>(mr, a, st);
+        case 8: return launch_mr<8, NA>(mr, a, st);
     }
     return 0;
 }
@@ -280,7 +285,7 @@ int pick_e(int L) {
 
 int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
     if (fmt != OFS_C64 || precision != OFS_FP32) return 0;
-    if (n_ant != 1) return 0;
+    if (n_ant != 1 && n_ant != 2) return 0;
     if (T < 2 || T > TMAX || (T & 1)) return 0;
     if (L < 128 || L > TMAX) return 0;
     const int E = pick_e(L);
@@ -291,5 +296,5 @@ int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
     const int plan = ofs_aa_fast_plan(fmt, precision, n_ant, a.T, a.L);
     if (!plan) return 0;
-    return launch_e(plan / 10, plan % 10, a, st);
+    return n_ant == 1 ? launch_e<1>(plan / 10, plan % 10, a, st) : launch_e<2>(plan / 10, plan % 10, a, st);
 }

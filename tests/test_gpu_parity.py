@@ -516,3 +516,28 @@ def test_receiver_backend_batched_vs_oracle(fmt, nb, N):
         assert relerr(out["h"][b].cpu().numpy(), r["h"]) < 1e-9
         assert relerr(out["xa"][b].cpu().numpy(), r["xa"]) < 1e-8
         assert abs(out["evm"][b].item() - r["evm"]) < 1e-8 * max(1.0, r["evm"])
+
+
+@pytest.mark.parametrize("T,L", [(1024, 512), (1024, 128), (768, 256)])
+def test_aa_fp32_fast_path_two_antennas(T, L):
+    """Register-staged fast kernel with two antennas (products and energies summed over the
+    antennas, sync_aa.py:463-480): metric within 1e-6, events as the fp32 single-antenna path."""
+    assert _lib.lib().ofs_aa_plan(_lib.C64, _lib.FP32, 2, T, L) >= 1000
+    rng = np.random.default_rng(T + L)
+    B = 24
+    x = (rng.standard_normal((B, 2, T)) + 1j * rng.standard_normal((B, 2, T))) * 0.5
+    for b in range(0, B, 2):
+        s = int(rng.integers(0, T - 2 * L + 1))
+        a = rng.standard_normal((2, L)) + 1j * rng.standard_normal((2, L))
+        x[b, :, s:s + L] += 2 * a
+        x[b, :, s + L:s + 2 * L] += 2 * a
+    x = x.astype(np.complex64)
+    out = sync_aa.aa_detect_streaming_batched(torch.from_numpy(x).cuda(), L=L, precision="fp32")
+    nev = out.n_events.cpu().numpy()
+    for b in range(B):
+        Pr, Rr, Mr, vr, ei, er = O.aa_detect(x[b].astype(np.complex128), L)
+        assert np.max(np.abs(out.M[b].cpu().numpy() - Mr)) < 1e-6
+        assert relerr(out.P[b].cpu().numpy(), Pr) < 1e-5 and relerr(out.R[b].cpu().numpy(), Rr) < 1e-5
+        assert nev[b] == len(ei)
+        for (pk, gs, ge, _), got in zip(ei, out.ev_int[b, :nev[b]].cpu().numpy()):
+            assert abs(got[1] - gs) <= 1 and abs(got[2] - ge) <= 1 and abs(got[0] - pk) <= 2

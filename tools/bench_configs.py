@@ -189,7 +189,29 @@ def backend(dev, st, steps, warmup):
                 frames_per_s=round(B / (ms / 1e3), 1))
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
+def cfg3_2ant(dev, st, steps, warmup):
+    """cfg3 with two receive antennas per stream (sync_aa's run_single_test uses 2 RX): 65536 x
+    2 x 1024 c64, L=512, fp32 fast path, events fused."""
+    B, T, L, E = 65536, 1024, 512, 4
+    x = synth.synth_batch(synth.faded_base(L, "cir1", (0, 1)), B, T, seed=32, device=dev)
+    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
+    R = torch.empty((B, T), dtype=torch.float32, device=dev)
+    M = torch.empty_like(R)
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), B, 2, T, L, _lib.FP32, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa 2ant"), steps, warmup, st)
+    plan = L_.ofs_aa_plan(_lib.C64, _lib.FP32, 2, T, L)
+    return dict(config="cfg3_2ant", workload=f"sync_aa S&C fp32, L={L}, {B} streams x 2 antennas x {T} c64",
+                kernel=f"aa_fast_kernel<E={(plan - 1000) // 10},MR={plan % 10},NA=2>" if plan >= 1000 else str(plan),
+                samples=B * 2 * T, ms=ms, alg_bytes=B * T * (16 + 16) + B * 4,
+                bytes_per_sample="2 x 8 in + P 8 + R 4 + M 4 per time index")
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
 
 
 def main():
