@@ -29,7 +29,7 @@ namespace {
 constexpr int WF_WG = 256;            // 4 waves = 4 streams per workgroup
 enum { WF_SC = 1, WF_COMB = 2, WF_MINN = 3 };
 
-template <int MODE, int E, int MW>
+template <int MODE, int E, int MW, int NB>
 __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     constexpr int RL = 64 * E;
     constexpr int W = MW * RL;
@@ -44,12 +44,12 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
     const int nrows = (int)((T + RL - 1) / RL);
-    const float4* xs = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(a.x) + b * T);
+    const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
     float* Mo = reinterpret_cast<float*>(a.M) + b * nout;
     float2* Po = reinterpret_cast<float2*>(a.P) + b * nout;
     float* Ro = reinterpret_cast<float*>(a.R) + b * nout;
 
-    float lr[MW][E], li[MW][E];                  // x of rows k-MW..k-1 (lag D = W)
+    float lr[NB][MW][E], li[NB][MW][E];          // x of rows k-MW..k-1 (lag D = W), per branch
     float sR[MW][E], sI[MW][E], sE[MW][E];       // retained in-window suffixes
     float hR[HR][E], hI[HR][E], hE[HR][E];       // window sums of past rows (COMB/MINN)
     double cbR[MW], cbI[MW], cbE[MW];            // row bases C[j] for j in (k-MW, k]
@@ -58,20 +58,28 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     for (int m = 0; m < MW; ++m) {
         cbR[m] = 0.0; cbI[m] = 0.0; cbE[m] = 0.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { lr[m][e] = 0.f; li[m][e] = 0.f; sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f; }
+        for (int e = 0; e < E; ++e) {
+            sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f;
+#pragma unroll
+            for (int t = 0; t < NB; ++t) { lr[t][m][e] = 0.f; li[t][m][e] = 0.f; }
+        }
     }
 #pragma unroll
     for (int m = 0; m < HR; ++m)
 #pragma unroll
         for (int e = 0; e < E; ++e) { hR[m][e] = 0.f; hI[m][e] = 0.f; hE[m][e] = 0.f; }
 
-    float4 nx[PD][V4];
-    auto load_row = [&](int k, float4 (&dst)[V4]) {
+    float4 nx[PD][NB][V4];
+    auto load_row = [&](int k, float4 (&dst)[NB][V4]) {
 #pragma unroll
-        for (int j = 0; j < V4; ++j) {
-            int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;       // float4 index (2 samples)
-            const int64_t qmax = T / 2 - 1;
-            dst[j] = xs[q < qmax ? q : qmax];                       // zeroed on use past T
+        for (int t = 0; t < NB; ++t) {
+            const float4* xs = reinterpret_cast<const float4*>(xb + (int64_t)t * T);
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;   // float4 index (2 samples)
+                const int64_t qmax = T / 2 - 1;
+                dst[t][j] = xs[q < qmax ? q : qmax];                // zeroed on use past T
+            }
         }
     };
 #pragma unroll
@@ -83,29 +91,32 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
             const int k = k0 + u;
             if (k < nrows) {
                 const int64_t nb = (int64_t)RL * k + E * lane;
-                float cr[E], ci[E];
-#pragma unroll
-                for (int j = 0; j < V4; ++j) {
-                    const bool ok = nb + 2 * j < T;                 // T even: pairs are whole
-                    const float4 v = nx[u % PD][j];
-                    cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
-                    cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
-                }
-                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);   // PD rows ahead
-                // ---- lagged products and energies (fp32) ----
                 const int sl = u % MW;                              // ring slot of row k (and k-MW)
+                // ---- lagged products and energies (fp32), summed over the branches ----
                 float aR[E], aI[E], aE[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    aE[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
-                    if (k >= MW) {
-                        aR[e] = fmaf(cr[e], lr[sl][e], ci[e] * li[sl][e]);
-                        aI[e] = fmaf(ci[e], lr[sl][e], -(cr[e] * li[sl][e]));
-                    } else {
-                        aR[e] = 0.f; aI[e] = 0.f;
+                for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    float cr[E], ci[E];
+#pragma unroll
+                    for (int j = 0; j < V4; ++j) {
+                        const bool ok = nb + 2 * j < T;             // T even: pairs are whole
+                        const float4 v = nx[u % PD][t][j];
+                        cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
+                        cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
                     }
-                    lr[sl][e] = cr[e]; li[sl][e] = ci[e];
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        aE[e] += fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                        if (k >= MW) {
+                            aR[e] += fmaf(cr[e], lr[t][sl][e], ci[e] * li[t][sl][e]);
+                            aI[e] += fmaf(ci[e], lr[t][sl][e], -(cr[e] * li[t][sl][e]));
+                        }
+                        lr[t][sl][e] = cr[e]; li[t][sl][e] = ci[e];
+                    }
                 }
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);   // PD rows ahead
                 // ---- in-lane partials (forward f, backward g) ----
                 float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
                 fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
@@ -202,7 +213,7 @@ struct WinFusedArgs {
     float* Ms; float2* Ps; float* Rs; float* Mm; float2* Pm; float* Rm;
 };
 
-template <int E, int MW>
+template <int E, int MW, int NB>
 __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
     constexpr int RL = 64 * E;
     constexpr int N = 4 * MW * RL;
@@ -219,9 +230,9 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
     const int nrows = (int)((T + RL - 1) / RL);
-    const float4* xs = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(a.x) + b * T);
+    const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
 
-    float xr_[XR][E], xi_[XR][E];
+    float xr_[NB][XR][E], xi_[NB][XR][E];
     float shR[XR][E], shI[XR][E];               // S_h suffixes (window 2Q = XR rows)
     float sqR[MW][E], sqI[MW][E], seE[MW][E];   // S_q, S_e suffixes (window Q = MW rows)
     double chR[XR], chI[XR], cqR[MW], cqI[MW], ceE[MW];
@@ -230,7 +241,11 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
     for (int m = 0; m < XR; ++m) {
         chR[m] = 0; chI[m] = 0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { xr_[m][e] = 0.f; xi_[m][e] = 0.f; shR[m][e] = 0.f; shI[m][e] = 0.f; }
+        for (int e = 0; e < E; ++e) {
+            shR[m][e] = 0.f; shI[m][e] = 0.f;
+#pragma unroll
+            for (int t = 0; t < NB; ++t) { xr_[t][m][e] = 0.f; xi_[t][m][e] = 0.f; }
+        }
     }
 #pragma unroll
     for (int m = 0; m < MW; ++m) {
@@ -240,13 +255,17 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
     }
     auto H = [&](int row, int e) -> float& { return hist[w][row][e][lane]; };
 
-    float4 nx[PD][V4];
-    auto load_row = [&](int k, float4 (&dst)[V4]) {
+    float4 nx[PD][NB][V4];
+    auto load_row = [&](int k, float4 (&dst)[NB][V4]) {
 #pragma unroll
-        for (int j = 0; j < V4; ++j) {
-            const int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;
-            const int64_t qmax = T / 2 - 1;
-            dst[j] = xs[q < qmax ? q : qmax];
+        for (int t = 0; t < NB; ++t) {
+            const float4* xs = reinterpret_cast<const float4*>(xb + (int64_t)t * T);
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                const int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;
+                const int64_t qmax = T / 2 - 1;
+                dst[t][j] = xs[q < qmax ? q : qmax];
+            }
         }
     };
 #pragma unroll
@@ -273,26 +292,31 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
             const int k = k0 + u;
             if (k < nrows) {
                 const int64_t nb = (int64_t)RL * k + E * lane;
-                float cr[E], ci[E];
-#pragma unroll
-                for (int j = 0; j < V4; ++j) {
-                    const bool ok = nb + 2 * j < T;
-                    const float4 v = nx[u % PD][j];
-                    cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
-                    cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
-                }
-                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
                 const int x2 = u % XR;                 // row k-2MW (x ring), then row k
                 const int x1 = (u + MW) % XR;          // row k-MW
                 float hR[E], hI[E], qR[E], qI[E], en[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    en[e] = fmaf(cr[e], cr[e], ci[e] * ci[e]);
-                    const float d2r = xr_[x2][e], d2i = xi_[x2][e], d1r = xr_[x1][e], d1i = xi_[x1][e];
-                    hR[e] = fmaf(cr[e], d2r, ci[e] * d2i); hI[e] = fmaf(ci[e], d2r, -(cr[e] * d2i));
-                    qR[e] = fmaf(cr[e], d1r, ci[e] * d1i); qI[e] = fmaf(ci[e], d1r, -(cr[e] * d1i));
-                    xr_[x2][e] = cr[e]; xi_[x2][e] = ci[e];
+                for (int e = 0; e < E; ++e) { hR[e] = 0.f; hI[e] = 0.f; qR[e] = 0.f; qI[e] = 0.f; en[e] = 0.f; }
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {         // products summed over the branches
+                    float cr[E], ci[E];
+#pragma unroll
+                    for (int j = 0; j < V4; ++j) {
+                        const bool ok = nb + 2 * j < T;
+                        const float4 v = nx[u % PD][t][j];
+                        cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
+                        cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
+                    }
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        en[e] += fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                        const float d2r = xr_[t][x2][e], d2i = xi_[t][x2][e], d1r = xr_[t][x1][e], d1i = xi_[t][x1][e];
+                        hR[e] += fmaf(cr[e], d2r, ci[e] * d2i); hI[e] += fmaf(ci[e], d2r, -(cr[e] * d2i));
+                        qR[e] += fmaf(cr[e], d1r, ci[e] * d1i); qI[e] += fmaf(ci[e], d1r, -(cr[e] * d1i));
+                        xr_[t][x2][e] = cr[e]; xi_[t][x2][e] = ci[e];
+                    }
                 }
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
                 Part ph_r, ph_i, pq_r, pq_i, pe;
                 part(hR, ph_r); part(hI, ph_i); part(qR, pq_r); part(qI, pq_i); part(en, pe);
                 const int sq = u % MW, soq = (u + 1) % MW, soh = (u + 1) % XR;
@@ -359,29 +383,29 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
     }
 }
 
-template <int MODE, int E, int MW>
+template <int MODE, int E, int MW, int NB>
 int launch(const WinFastArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + 3) / 4;
-    hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
-template <int MODE, int E>
+template <int MODE, int E, int NB>
 int launch_mw(int mw, const WinFastArgs& a, hipStream_t st) {
     switch (mw) {
-        case 1: return launch<MODE, E, 1>(a, st);
-        case 2: return launch<MODE, E, 2>(a, st);
-        case 4: return launch<MODE, E, 4>(a, st);
-        case 8: return launch<MODE, E, 8>(a, st);
+        case 1: return launch<MODE, E, 1, NB>(a, st);
+        case 2: return launch<MODE, E, 2, NB>(a, st);
+        case 4: return launch<MODE, E, 4, NB>(a, st);
+        case 8: return launch<MODE, E, 8, NB>(a, st);
     }
     return 0;
 }
 
-template <int MODE>
+template <int MODE, int NB>
 int launch_e(int e, int mw, const WinFastArgs& a, hipStream_t st) {
     switch (e) {
-        case 2: return launch_mw<MODE, 2>(mw, a, st);
-        case 4: return launch_mw<MODE, 4>(mw, a, st);
+        case 2: return launch_mw<MODE, 2, NB>(mw, a, st);
+        case 4: return launch_mw<MODE, 4, NB>(mw, a, st);
     }
     return 0;
 }
@@ -399,17 +423,17 @@ void pick(int W, int& E, int& mw) {
         }
 }
 
-template <int E, int MW>
+template <int E, int MW, int NB>
 int launch_fused(const WinFusedArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + 3) / 4;
-    hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
 }  // namespace
 
 int ofs_sc_minn_fast_plan(int fmt, int precision, int n_br, int64_t T, int N) {
-    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br != 1 || (T & 1) || T < N || N % 4) return 0;
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || (T & 1) || T < N || N % 4) return 0;
     const int Q = N / 4;
     for (int e : {4, 2}) {                     // per-wave LDS history: 64·E·(8·MW) floats
         if (Q % (64 * e)) continue;
@@ -424,22 +448,32 @@ int ofs_sc_minn_fast_try(int fmt, int precision, int n_br, const void* x, int64_
     const int plan = ofs_sc_minn_fast_plan(fmt, precision, n_br, T, N);
     if (!plan) return 0;
     const WinFusedArgs a{x, B, T, N, (float*)Ms, (float2*)Ps, (float*)Rs, (float*)Mm, (float2*)Pm, (float*)Rm};
+    if (n_br == 2) {
+        switch (plan) {
+            case 41: return launch_fused<4, 1, 2>(a, st);
+            case 42: return launch_fused<4, 2, 2>(a, st);
+            case 21: return launch_fused<2, 1, 2>(a, st);
+            case 22: return launch_fused<2, 2, 2>(a, st);
+            default: return launch_fused<2, 4, 2>(a, st);
+        }
+    }
     switch (plan) {
-        case 41: return launch_fused<4, 1>(a, st);
-        case 42: return launch_fused<4, 2>(a, st);
-        case 21: return launch_fused<2, 1>(a, st);
-        case 22: return launch_fused<2, 2>(a, st);
-        default: return launch_fused<2, 4>(a, st);
+        case 41: return launch_fused<4, 1, 1>(a, st);
+        case 42: return launch_fused<4, 2, 1>(a, st);
+        case 21: return launch_fused<2, 1, 1>(a, st);
+        case 22: return launch_fused<2, 2, 1>(a, st);
+        default: return launch_fused<2, 4, 1>(a, st);
     }
 }
 
 int ofs_win_fast_plan(int mode, int fmt, int precision, int n_br, int64_t T, int N) {
-    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br != 1 || (T & 1) || T < N) return 0;
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || (T & 1) || T < N) return 0;
     if (mode < WF_SC || mode > WF_MINN) return 0;
     const int div = mode == WF_MINN ? 4 : 2;
     if (N % div) return 0;
     int E, mw;
     pick(N / div, E, mw);
+    if (n_br == 2 && mw == 8) return 0;         // the two-branch x ring would spill (general engine)
     return E ? 10 * E + mw : 0;
 }
 
@@ -447,9 +481,16 @@ int ofs_win_fast_try(int mode, int fmt, int precision, int n_br, const WinFastAr
     const int plan = ofs_win_fast_plan(mode, fmt, precision, n_br, a.T, a.N);
     if (!plan) return 0;
     const int E = plan / 10, mw = plan % 10;
+    if (n_br == 2) {
+        switch (mode) {
+            case WF_SC: return launch_e<WF_SC, 2>(E, mw, a, st);
+            case WF_COMB: return launch_e<WF_COMB, 2>(E, mw, a, st);
+            default: return launch_e<WF_MINN, 2>(E, mw, a, st);
+        }
+    }
     switch (mode) {
-        case WF_SC: return launch_e<WF_SC>(E, mw, a, st);
-        case WF_COMB: return launch_e<WF_COMB>(E, mw, a, st);
-        default: return launch_e<WF_MINN>(E, mw, a, st);
+        case WF_SC: return launch_e<WF_SC, 1>(E, mw, a, st);
+        case WF_COMB: return launch_e<WF_COMB, 1>(E, mw, a, st);
+        default: return launch_e<WF_MINN, 1>(E, mw, a, st);
     }
 }

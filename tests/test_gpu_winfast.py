@@ -70,7 +70,8 @@ def test_window_fast_path_covers_cfg4():
     L = _lib.lib()
     assert L.ofs_win_plan(2, _lib.C64, _lib.FP32, 1, 4096, 2048) > 0
     assert L.ofs_win_plan(3, _lib.C64, _lib.FP32, 1, 4096, 2048) > 0
-    assert L.ofs_win_plan(1, _lib.C64, _lib.FP32, 2, 4096, 2048) == 0      # 2 branches: general
+    assert L.ofs_win_plan(1, _lib.C64, _lib.FP32, 2, 4096, 2048) > 0       # 2 branches: fast too
+    assert L.ofs_win_plan(1, _lib.C64, _lib.FP32, 3, 4096, 2048) == 0      # 3 branches: general
     assert L.ofs_win_plan(1, _lib.C128, _lib.FP64, 1, 4096, 2048) == 0     # fp64: general
 
 
@@ -102,3 +103,26 @@ def test_fused_sc_minn_general_fallback_fp64():
         np.testing.assert_allclose(Mm[b].cpu().numpy(), Mo, rtol=1e-9, atol=1e-12)
         Mo, _, _ = O.comb_sc_metric(x[b], 256)
         np.testing.assert_allclose(Ms[b].cpu().numpy(), Mo, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["sc", "comb", "minn", "fused"])
+@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 3000), (512, 900)])
+def test_fast_paths_two_branches_vs_oracle(kind, N, T):
+    """Two receive branches summed inside the streaming fast kernels (the reference's 2-D input,
+    e.g. combined_sc_min.run_simulation on cir1[:2]): same tolerances as one branch."""
+    code = {"sc": 1, "comb": 2, "minn": 3, "fused": 4}[kind]
+    assert _lib.lib().ofs_win_plan(code, _lib.C64, _lib.FP32, 2, T, N) > 0
+    B = 5
+    x = synth.synth_batch(synth.faded_base(min(N // 2, 1024), "cir1", (0, 1)), B, T, seed=N + T)
+    xh = x.cpu().numpy().astype(np.complex128)
+    if kind == "fused":
+        (Mm, Pm, Rm), (Ms, Ps, Rs) = combined_sc_min.sc_minn_streaming_metrics_batched(x, N)
+        outs = [("minn", Mm, Pm, Rm), ("comb", Ms, Ps, Rs)]
+    else:
+        M, P, R = run(kind, x, N)
+        outs = [(kind, M, P, R)]
+    for k, M, P, R in outs:
+        for b in range(B):
+            Mo, Po, Ro = ORACLE[k](xh[b], N)
+            assert m_ok(M[b].cpu().numpy(), Mo)
+            assert relerr(P[b].cpu().numpy(), Po) < 1e-5 and relerr(R[b].cpu().numpy(), Ro) < 1e-5

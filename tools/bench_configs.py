@@ -211,7 +211,23 @@ def cfg3_2ant(dev, st, steps, warmup):
                 bytes_per_sample="2 x 8 in + P 8 + R 4 + M 4 per time index")
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
+def cfg4_2br(dev, st, steps, warmup):
+    """cfg4 with two receive branches per stream (combined_sc_min.run_simulation feeds cir1[:2]):
+    16384 x 2 x 4096 c64, N = 2048, fused S&C + Minn."""
+    B, T, N = 16384, 4096, 2048
+    x = synth.synth_batch(synth.faded_base(N // 2, "cir1", (0, 1)), B, T, seed=42, device=dev)
+    n_out = T - N + 1
+    outs = [torch.empty((B, n_out), dtype=dt, device=dev) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    L_ = _lib.lib()
+    ms = timed(lambda: chk(L_.ofs_sc_minn_metric(_lib.C64, x.data_ptr(), B, 2, T, N, _lib.FP32,
+                                                 *[t.data_ptr() for t in outs], st.cuda_stream), "sc_minn 2br"),
+               steps, warmup, st)
+    return dict(config="cfg4_2br", workload=f"combined_sc_min S&C + Minn, N={N}, {B} x 2 branches x {T} c64, fp32",
+                kernel="sc_minn_fast_kernel<NB=2> (fused, one pass)", samples=B * 2 * T, ms=ms,
+                alg_bytes=B * 2 * T * 8 + 2 * B * n_out * 16, bytes_per_sample="2 x 8 in + 2 x 16 per output")
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
 
 
 def main():
