@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--max-events", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--alloc", choices=("contiguous", "plain"), default="contiguous",
+                    help="batch arena backing: hipDeviceMallocContiguous or a plain allocation")
     return ap.parse_args()
 
 
@@ -108,7 +110,8 @@ def main():
     # input and outputs of one batch live in ONE device allocation (_lib.arena);
     # the synthetic batch is generated, then copied in
     x, P, R, M = _lib.arena(dev, [((B, 1, T), torch.complex64), ((B, T), torch.complex64),
-                                  ((B, T), torch.float32), ((B, T), torch.float32)])
+                                  ((B, T), torch.float32), ((B, T), torch.float32)],
+                            contiguous=a.alloc == "contiguous")
     x.copy_(synth.make_aa_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev))
     torch.cuda.empty_cache()
     n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)

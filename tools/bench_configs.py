@@ -227,7 +227,28 @@ def cfg4_2br(dev, st, steps, warmup):
                 alg_bytes=B * 2 * T * 8 + 2 * B * n_out * 16, bytes_per_sample="2 x 8 in + 2 x 16 per output")
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
+def cfg3_fp64(dev, st, steps, warmup):
+    """cfg3 shape in the reference's float64 (complex128 in, f64/c128 out: the numpy drop-in's
+    precision), 65536 x 1024, L = 512, events fused."""
+    B, T, L, E = 65536, 1024, 512, 4
+    x = synth.make_aa_batch(B, T, L, seed=33, device=dev, dtype=torch.complex128)
+    P = torch.empty((B, T), dtype=torch.complex128, device=dev)
+    R = torch.empty((B, T), dtype=torch.float64, device=dev)
+    M = torch.empty_like(R)
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C128, x.data_ptr(), B, 1, T, L, _lib.FP64, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa fp64"), steps, warmup, st)
+    plan = L_.ofs_aa_plan(_lib.C128, _lib.FP64, 1, T, L)
+    return dict(config="cfg3_fp64", workload=f"sync_aa S&C fp64, L={L}, {B} x {T} c128", kernel=f"plan {plan}",
+                samples=B * T, ms=ms, alg_bytes=B * T * (16 + 16 + 8 + 8) + B * 4,
+                bytes_per_sample="16 in + P 16 + R 8 + M 8")
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
 
 
 def main():
