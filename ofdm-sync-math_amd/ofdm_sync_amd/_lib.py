@@ -223,7 +223,7 @@ class _DeviceBlock:
 HIP_MALLOC_CONTIGUOUS = 0x4           # hipDeviceMallocContiguous (hip_runtime_api.h)
 
 
-def arena(dev, specs, contiguous: bool = False):
+def arena(dev, specs, contiguous: bool = False, gap: int = 0):
     """Carve several output tensors out of ONE device allocation.
 
     specs: list of (shape, dtype) or None.  Buffers of >= 2 MiB start on 2 MiB boundaries,
@@ -243,7 +243,7 @@ def arena(dev, specs, contiguous: bool = False):
         al = big if n >= big else 256
         total = (total + al - 1) // al * al
         offs.append((total, n, shape, dtype))
-        total += n
+        total += n + (gap if n >= big else 0)
     if total == 0:
         return [None if o is None else torch.empty(o[2], dtype=o[3], device=dev) for o in offs]
     if contiguous:

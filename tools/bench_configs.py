@@ -40,6 +40,19 @@ def timed(step, steps, warmup, stream):
     return e0.elapsed_time(e1) / steps
 
 
+def batch_arena(dev, specs, contiguous):
+    """Input + outputs of a config in one allocation; physically contiguous where measured
+    faster (cfg5: 6.05 vs 6.14 ms; cfg4 is the opposite - 1.41 vs 0.69-0.75 ms with its 7
+    streams - and keeps separate allocations),
+    falling back to a plain allocation if the driver cannot provide a contiguous one."""
+    if contiguous:
+        try:
+            return _lib.arena(dev, specs, contiguous=True)
+        except MemoryError:
+            pass
+    return _lib.arena(dev, specs, contiguous=False)
+
+
 def chk(rc, what):
     if rc:
         raise RuntimeError(f"{what}: status {rc}")
@@ -139,9 +152,12 @@ def cfg5(dev, st, steps, warmup, n_seq=1 << 20):
     """cfg5: zc_freq metric, N=4096, one window per sequence (cp=0), 1M sequences x 4096 c64."""
     N = 4096
     g = torch.Generator(device=dev).manual_seed(5)
-    x = torch.randn((n_seq, N), dtype=torch.complex64, device=dev, generator=g)
     prec = int(os.environ.get("OFS_CFG5_PREC", "0"))           # 0 fp32 window FFT, 1 fp64 sliding DFT
-    out = torch.empty((n_seq, 1), dtype=torch.float32 if prec == 0 else torch.float64, device=dev)
+    x, out = batch_arena(dev, [((n_seq, N), torch.complex64),
+                               ((n_seq, 1), torch.float32 if prec == 0 else torch.float64)], contiguous=True)
+    for i in range(0, n_seq, 1 << 17):                          # fill in chunks (no 32 GiB temporary)
+        x[i:i + (1 << 17)].copy_(torch.randn((min(1 << 17, n_seq - i), N), dtype=torch.complex64, device=dev,
+                                             generator=g))
     idx, t, e = zc_freq.make_pss_frequency_template()
     idx32 = np.ascontiguousarray(idx.astype(np.int32))
     tb = np.ascontiguousarray(t.astype(np.complex128))
