@@ -42,6 +42,7 @@ extern "C" {
 #define OFS_ETOOLONG     -2   /* window/halo does not fit one workgroup's LDS tile          */
 #define OFS_EHIP         -3   /* kernel launch failed (hipGetLastError)                     */
 #define OFS_ESHORT       -4   /* stream shorter than one symbol (zc_freq.py:76-78 raises)   */
+#define OFS_EFFT         -5   /* rocFFT plan creation / execution failed                    */
 
 /* ofs_zc_correlate modes */
 #define OFS_ZC_RAW        0   /* per-branch np.convolve(x, conj(ref[::-1]))                 */
@@ -271,6 +272,37 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
  * window FFT with the column sums reduced across lanes (fp32; taken when the template bins'
  * residues mod 64 are distinct, as the PSS template's are, otherwise 2), 0 none */
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp);
+
+/*
+ * rocFFT leg of the ZC frequency-domain metric (zc_freq.py:62-99 and the argmax of
+ * zc_freq.py:144), the north-star "rocFFT + HIP conj-mul/|.|^2/argmax" formulation, kept beside
+ * the fused window-FFT kernel of ofs_zc_freq_metric for comparison (it writes and re-reads the
+ * full spectrum).  A plan is a batched forward C2C rocFFT plan over n_windows = B * n_br windows
+ * of N samples, input distance in_dist (= T), out-of-place into a dense [n_windows][N] spectrum;
+ * it is host state owned by the caller (create once per shape, destroy when done).
+ *   precision OFS_FP32: complex64 input/spectrum, f32 metric; OFS_FP64: complex128, f64 metric.
+ *   work_bytes: size of the rocFFT work buffer the caller passes to ofs_zc_freq_metric_fft.
+ */
+int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                               void** plan, size_t* work_bytes);
+int32_t ofs_zc_fft_plan_destroy(void* plan);
+/*
+ * For each offset off in [0, T-(N+cp)]: one batched rocFFT of x[b][br][off+cp : off+cp+N] into
+ * `spectrum` ([B*n_br][N], device scratch), then one gather kernel: metric[b][off] =
+ * |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum |bins|^2, 1e-12), bins at the reference's
+ * fftshift positions (N/2 + bin_indices) % N.  bin_indices [n_bins] int32, template_bins [n_bins]
+ * c128: HOST pointers (n_bins <= 64).  metric [B][n_off]; peak_index [B] int64 / peak_value [B]
+ * f64 (nullable) = first argmax of each row (np.argmax).  Returns OFS_ESHORT when T < N + cp.
+ */
+int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
+                               int64_t T, int32_t N, int32_t cp, int32_t n_bins,
+                               const int32_t* bin_indices, const double* template_bins,
+                               double template_energy, void* spectrum, void* work, void* metric,
+                               int64_t* peak_index, double* peak_value, void* stream);
+/* first argmax of each row of v [B][n] (f32 | f64 per precision), np.argmax semantics (the first
+ * maximal element; the first NaN if any): index [B] int64, value [B] f64, each nullable. */
+int32_t ofs_row_argmax(int32_t precision, const void* v, int64_t B, int64_t n, int64_t* index,
+                       double* value, void* stream);
 
 /*
  * ZC CFAR + gate: replaces zc_v2.zc_streaming_detection (zc_v2.py:300-346) fused with

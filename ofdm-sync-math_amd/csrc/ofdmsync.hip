@@ -814,6 +814,7 @@ const char* ofs_status_string(int32_t s) {
         case OFS_ETOOLONG: return "window/halo does not fit one LDS tile";
         case OFS_EHIP: return "HIP launch error";
         case OFS_ESHORT: return "stream shorter than one symbol";
+        case OFS_EFFT: return "rocFFT error";
         default: return "unknown status";
     }
 }

@@ -1,0 +1,251 @@
+// zc_rocfft.hip — the rocFFT leg of zc_freq.compute_frequency_metric (zc_freq.py:62-99).
+//
+// The north-star formulation of the ZC frequency-domain path: one library FFT per window
+// (rocFFT, batched over every stream x branch of one offset) followed by a hand-written
+// gather / conj-multiply / |.|^2 / normalise kernel, and a first-argmax kernel for the
+// reference's `peak_index = int(np.argmax(metric))` (zc_freq.py:144).
+//
+// It is the comparison path for the fused window-FFT kernel of corr.hip (zc_win64_kernel):
+// rocFFT must write the whole N-point spectrum of every window (8 B/bin fp32) and the gather
+// reads 62 bins of it back, so per window it moves 2 x 8N bytes against the fused kernel's
+// 8N (SURVEY §8d "report both").  Both are measured by tools/bench_configs.py (cfg5 / cfg5_rocfft).
+//
+// Index convention: the reference takes bins = fftshift(X)[(N/2 + idx) % N]; fftshift is
+// roll(X, N//2), so bin k is X[((N/2 + idx_k) % N - N//2) mod N] of the unshifted spectrum.
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+#include <stdint.h>
+#include <math.h>
+#include <mutex>
+#include "ofdmsync.h"
+
+namespace {
+
+constexpr int ZB = 64;          // max template bins (one lane each)
+constexpr int ZWG = 256;        // 4 waves = 4 streams per workgroup
+
+struct ZcFftPlan {
+    rocfft_plan plan = nullptr;
+    int32_t precision = 0;
+    int32_t N = 0;
+    int64_t n_windows = 0;
+    int64_t in_dist = 0;
+    size_t work_bytes = 0;
+};
+
+struct GatherArgs {
+    const void* spec;           // [B][n_br][N] c64 | c128 (unshifted spectrum of one offset)
+    int64_t B, n_off, off;
+    int32_t n_br, N, n_bins;
+    double e_t;
+    void* metric;               // [B][n_off] f32 | f64
+    int32_t pos[ZB];            // unshifted spectrum index of template bin k
+    double t_re[ZB], t_im[ZB];  // template bins
+};
+
+// One wave per stream: lane k owns template bin k; sum_br vdot(t, bins) and sum_br sum |bins|^2
+// are accumulated in fp64 (zc_freq.py:88-95) and reduced across the wave.
+template <class R>
+__global__ __launch_bounds__(ZWG) void zc_gather_kernel(GatherArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * (ZWG / 64) + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    double cr = 0.0, ci = 0.0, en = 0.0;
+    if (lane < a.n_bins) {
+        const int p = a.pos[lane];
+        const double tr = a.t_re[lane], ti = a.t_im[lane];
+        for (int br = 0; br < a.n_br; ++br) {
+            const int64_t i = ((b * a.n_br + br) * (int64_t)a.N + p);
+            double xr, xi;
+            if constexpr (sizeof(R) == 4) {
+                const float2 v = reinterpret_cast<const float2*>(a.spec)[i];
+                xr = v.x; xi = v.y;
+            } else {
+                const double2 v = reinterpret_cast<const double2*>(a.spec)[i];
+                xr = v.x; xi = v.y;
+            }
+            cr += tr * xr + ti * xi;                     // conj(t) * x
+            ci += tr * xi - ti * xr;
+            en += xr * xr + xi * xi;
+        }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        cr += __shfl_xor(cr, m);
+        ci += __shfl_xor(ci, m);
+        en += __shfl_xor(en, m);
+    }
+    if (lane == 0) {
+        const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
+        if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[b * a.n_off + a.off] = (float)v;
+        else reinterpret_cast<double*>(a.metric)[b * a.n_off + a.off] = v;
+    }
+}
+
+// First argmax of each row (np.argmax: the first maximal element; a NaN wins at its first
+// occurrence, as numpy's does).  One wave per row.
+template <class R>
+__global__ __launch_bounds__(ZWG) void row_argmax_kernel(const R* __restrict__ v, int64_t B, int64_t n,
+                                                        int64_t* __restrict__ idx, double* __restrict__ val) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * (ZWG / 64) + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const R* row = v + b * n;
+    double best = -INFINITY;
+    int64_t bi = n;                                     // sentinel: nothing seen
+    bool nan_seen = false;
+    for (int64_t j = lane; j < n; j += 64) {
+        const double x = (double)row[j];
+        if (x != x) { if (!nan_seen) { nan_seen = true; best = x; bi = j; } }
+        else if (!nan_seen && (x > best || bi == n)) { best = x; bi = j; }
+    }
+    // combine: a NaN beats any number (earliest NaN), otherwise larger value, then smaller index
+    for (int m = 32; m >= 1; m >>= 1) {
+        const double ob = __shfl_xor(best, m);
+        const int64_t oi = __shfl_xor(bi, m);
+        const bool on = __shfl_xor((int)nan_seen, m) != 0;
+        bool take;
+        if (oi == n) take = false;
+        else if (bi == n) take = true;
+        else if (on != nan_seen) take = on;
+        else if (on) take = oi < bi;
+        else take = (ob > best) || (ob == best && oi < bi);
+        if (take) { best = ob; bi = oi; nan_seen = on; }
+    }
+    if (lane == 0) {
+        if (idx) idx[b] = bi == n ? 0 : bi;
+        if (val) val[b] = best;
+    }
+}
+
+std::once_flag g_setup;
+
+}  // namespace
+
+extern "C" {
+
+int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                               void** plan_out, size_t* work_bytes) {
+    if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || n_windows < 1 ||
+        in_dist < N)
+        return OFS_EINVAL;
+    *plan_out = nullptr;
+    std::call_once(g_setup, [] { rocfft_setup(); });
+    rocfft_plan_description desc = nullptr;
+    if (rocfft_plan_description_create(&desc) != rocfft_status_success) return OFS_EFFT;
+    const size_t len = (size_t)N, stride = 1;
+    rocfft_status s = rocfft_plan_description_set_data_layout(
+        desc, rocfft_array_type_complex_interleaved, rocfft_array_type_complex_interleaved, nullptr, nullptr,
+        1, &stride, (size_t)in_dist, 1, &stride, (size_t)N);
+    ZcFftPlan* p = new ZcFftPlan;
+    if (s == rocfft_status_success)
+        s = rocfft_plan_create(&p->plan, rocfft_placement_notinplace, rocfft_transform_type_complex_forward,
+                               precision == OFS_FP32 ? rocfft_precision_single : rocfft_precision_double, 1, &len,
+                               (size_t)n_windows, desc);
+    rocfft_plan_description_destroy(desc);
+    if (s == rocfft_status_success) s = rocfft_plan_get_work_buffer_size(p->plan, &p->work_bytes);
+    if (s != rocfft_status_success) {
+        if (p->plan) rocfft_plan_destroy(p->plan);
+        delete p;
+        return OFS_EFFT;
+    }
+    p->precision = precision;
+    p->N = N;
+    p->n_windows = n_windows;
+    p->in_dist = in_dist;
+    if (work_bytes) *work_bytes = p->work_bytes;
+    *plan_out = p;
+    return OFS_OK;
+}
+
+int32_t ofs_zc_fft_plan_destroy(void* plan) {
+    ZcFftPlan* p = static_cast<ZcFftPlan*>(plan);
+    if (!p) return OFS_OK;
+    if (p->plan) rocfft_plan_destroy(p->plan);
+    delete p;
+    return OFS_OK;
+}
+
+int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                               int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
+                               const double* template_bins, double template_energy, void* spectrum, void* work,
+                               void* metric, int64_t* peak_index, double* peak_value, void* stream) {
+    ZcFftPlan* p = static_cast<ZcFftPlan*>(plan);
+    if (!p || !x || !spectrum || !metric || !bin_indices || !template_bins || B < 0 || n_br < 1 || T < 0 ||
+        N < 1 || cp < 0 || n_bins < 1 || n_bins > ZB)
+        return OFS_EINVAL;
+    const int32_t want_fmt = p->precision == OFS_FP32 ? OFS_C64 : OFS_C128;
+    if (in_fmt != want_fmt || p->N != N || p->in_dist != T || p->n_windows != B * (int64_t)n_br) return OFS_EINVAL;
+    if (p->work_bytes && !work) return OFS_EINVAL;
+    if (T < (int64_t)N + cp) return OFS_ESHORT;
+    if (B == 0) return OFS_OK;
+    const int64_t n_off = T - ((int64_t)N + cp) + 1;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+
+    GatherArgs g{};
+    g.spec = spectrum;
+    g.B = B;
+    g.n_off = n_off;
+    g.n_br = n_br;
+    g.N = N;
+    g.n_bins = n_bins;
+    g.e_t = template_energy;
+    g.metric = metric;
+    const int64_t dc = N / 2;
+    for (int k = 0; k < n_bins; ++k) {
+        const int64_t pos = (((dc + bin_indices[k]) % N) + N) % N;          // zc_freq.py:80
+        g.pos[k] = (int32_t)((((pos - N / 2) % N) + N) % N);               // undo fftshift
+        g.t_re[k] = template_bins[2 * k];
+        g.t_im[k] = template_bins[2 * k + 1];
+    }
+
+    rocfft_execution_info info = nullptr;
+    if (rocfft_execution_info_create(&info) != rocfft_status_success) return OFS_EFFT;
+    rocfft_status s = rocfft_execution_info_set_stream(info, st);
+    if (s == rocfft_status_success && p->work_bytes)
+        s = rocfft_execution_info_set_work_buffer(info, work, p->work_bytes);
+    const size_t esz = p->precision == OFS_FP32 ? 8 : 16;
+    const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
+    int32_t rc = OFS_OK;
+    for (int64_t off = 0; off < n_off && s == rocfft_status_success; ++off) {
+        // windows x[b][br][off+cp : off+cp+N], distance T: one batched transform per offset
+        void* in[1] = {const_cast<char*>(static_cast<const char*>(x)) + (size_t)(off + cp) * esz};
+        void* out[1] = {spectrum};
+        s = rocfft_execute(p->plan, in, out, info);
+        if (s != rocfft_status_success) break;
+        g.off = off;
+        if (p->precision == OFS_FP32) hipLaunchKernelGGL(zc_gather_kernel<float>, dim3(grid), dim3(ZWG), 0, st, g);
+        else hipLaunchKernelGGL(zc_gather_kernel<double>, dim3(grid), dim3(ZWG), 0, st, g);
+        if (hipGetLastError() != hipSuccess) { rc = OFS_EHIP; break; }
+    }
+    rocfft_execution_info_destroy(info);
+    if (s != rocfft_status_success) return OFS_EFFT;
+    if (rc) return rc;
+    if (peak_index || peak_value) {
+        if (p->precision == OFS_FP32)
+            hipLaunchKernelGGL(row_argmax_kernel<float>, dim3(grid), dim3(ZWG), 0, st,
+                               static_cast<const float*>(metric), B, n_off, peak_index, peak_value);
+        else
+            hipLaunchKernelGGL(row_argmax_kernel<double>, dim3(grid), dim3(ZWG), 0, st,
+                               static_cast<const double*>(metric), B, n_off, peak_index, peak_value);
+        if (hipGetLastError() != hipSuccess) return OFS_EHIP;
+    }
+    return OFS_OK;
+}
+
+int32_t ofs_row_argmax(int32_t precision, const void* v, int64_t B, int64_t n, int64_t* index, double* value,
+                       void* stream) {
+    if ((precision != OFS_FP32 && precision != OFS_FP64) || !v || B < 0 || n < 1 || (!index && !value))
+        return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (precision == OFS_FP32)
+        hipLaunchKernelGGL(row_argmax_kernel<float>, dim3(grid), dim3(ZWG), 0, st, static_cast<const float*>(v), B, n,
+                           index, value);
+    else
+        hipLaunchKernelGGL(row_argmax_kernel<double>, dim3(grid), dim3(ZWG), 0, st, static_cast<const double*>(v), B,
+                           n, index, value);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+}  // extern "C"

@@ -113,7 +113,9 @@ def aa_detect_streaming_batched(x, L: int = PREAMBLE_HALF_LEN, threshold: float 
     batch = _lib.as_batch(x, batched=True)
     prec = _lib.resolve_precision(batch, precision)
     want = tuple(outputs)
-    if detect and batch.T > 0:
+    # events on a multi-tile stream of the general engine (plan 2) are found in a second pass
+    # over P/M in HBM; every other plan keeps them on chip, so detect-only skips those stores
+    if detect and batch.T > 0 and _lib.lib().ofs_aa_plan(batch.fmt, prec, batch.nb, batch.T, int(L)) == 2:
         want = tuple(sorted(set(want) | {"P", "M"}, key=["P", "R", "M", "valid"].index))
     res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, max_events)
     if detect and batch.B > 0 and batch.T > 0:

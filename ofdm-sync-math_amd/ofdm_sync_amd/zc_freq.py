@@ -85,3 +85,96 @@ def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, te
     batch = _lib.as_batch(x, batched=True)
     return _run(batch, int(N_FFT if N is None else N), int(CYCLIC_PREFIX if cp is None else cp),
                 bin_indices, template_bins, template_energy, precision)
+
+
+# ------------------------------------------------------------------------------------------
+# rocFFT leg (include/ofdmsync.h ofs_zc_freq_metric_fft): batched rocFFT per offset + HIP
+# gather / conj-mul / |.|^2 / normalise kernel + first-argmax kernel.  Writes and re-reads the
+# full spectrum, so it is the comparison path for the fused window-FFT kernel above.
+# ------------------------------------------------------------------------------------------
+class FFTPlan:
+    """Caller-owned rocFFT plan for ``n_windows`` windows of ``N`` samples at distance ``T``."""
+
+    def __init__(self, precision: int, N: int, n_windows: int, T: int):
+        import ctypes
+        self._lib = _lib.lib()
+        h = ctypes.c_void_p()
+        wb = ctypes.c_size_t()
+        _lib.check(self._lib.ofs_zc_fft_plan_create(int(precision), int(N), int(n_windows), int(T),
+                                                   ctypes.byref(h), ctypes.byref(wb)), "ofs_zc_fft_plan_create")
+        self.handle, self.work_bytes = h.value, int(wb.value)
+        self.key = (int(precision), int(N), int(n_windows), int(T))
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h:
+            self._lib.ofs_zc_fft_plan_destroy(h)
+
+
+_plans: dict = {}
+
+
+def _plan(precision: int, N: int, n_windows: int, T: int) -> FFTPlan:
+    key = (precision, N, n_windows, T)
+    p = _plans.get(key)
+    if p is None:
+        if len(_plans) >= 8:
+            _plans.clear()
+        p = _plans[key] = FFTPlan(precision, N, n_windows, T)
+    return p
+
+
+def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
+                                            N: int | None = None, cp: int | None = None, *,
+                                            return_peak: bool = False):
+    """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
+    batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
+    complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
+    per-stream ``peak_index`` (int64, np.argmax of zc_freq.py:144) and peak value (f64)."""
+    if bin_indices is None:
+        bin_indices, template_bins, template_energy = make_pss_frequency_template()
+    batch = _lib.as_batch(x, batched=True)
+    if batch.fmt == _lib.CI16:
+        raise ValueError("the rocFFT leg takes complex64 or complex128 input")
+    N = int(N_FFT if N is None else N)
+    cp = int(CYCLIC_PREFIX if cp is None else cp)
+    idx = np.ascontiguousarray(np.asarray(bin_indices).astype(np.int32))
+    tb = np.ascontiguousarray(np.asarray(template_bins, dtype=np.complex128))
+    if idx.ndim != 1 or tb.shape != idx.shape or not 0 < idx.size <= 64:
+        raise ValueError("bin_indices and template_bins must be 1-D of equal length (1..64)")
+    noff = batch.T - (N + cp) + 1
+    if noff <= 0:
+        raise ValueError("Received stream is shorter than a single OFDM symbol.")
+    prec = _lib.FP32 if batch.fmt == _lib.C64 else _lib.FP64
+    dev = batch.data.device
+    plan = _plan(prec, N, batch.B * batch.nb, batch.T)
+    spec = torch.empty((batch.B * batch.nb, N), dtype=batch.data.dtype, device=dev)
+    work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
+    out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
+    pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None
+    pv = torch.empty((batch.B,), dtype=torch.float64, device=dev) if return_peak else None
+    rc = _lib.lib().ofs_zc_freq_metric_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
+                                           batch.T, N, cp, int(idx.size), idx.ctypes.data, tb.ctypes.data,
+                                           float(template_energy), spec.data_ptr(), _lib.ptr(work),
+                                           out.data_ptr(), _lib.ptr(pk), _lib.ptr(pv), _lib.stream_ptr())
+    _lib.check(rc, "ofs_zc_freq_metric_fft")
+    return (out, pk, pv) if return_peak else out
+
+
+def peak_index_batched(metric: torch.Tensor):
+    """Per-row first argmax of a device metric [B, n] (zc_freq.py:144 ``int(np.argmax(metric))``),
+    on the GPU: returns (index int64 [B], value f64 [B])."""
+    if metric.dim() == 1:
+        metric = metric[None]
+    if metric.dtype not in (torch.float32, torch.float64) or metric.device.type != "cuda":
+        raise ValueError("metric must be a float32/float64 CUDA tensor")
+    metric = metric.contiguous()
+    B, n = metric.shape
+    idx = torch.empty((B,), dtype=torch.int64, device=metric.device)
+    val = torch.empty((B,), dtype=torch.float64, device=metric.device)
+    if n == 0:
+        raise ValueError("attempt to get argmax of an empty sequence")
+    prec = _lib.FP32 if metric.dtype == torch.float32 else _lib.FP64
+    _lib.check(_lib.lib().ofs_row_argmax(prec, metric.data_ptr(), B, n, idx.data_ptr(), val.data_ptr(),
+                                         _lib.stream_ptr()), "ofs_row_argmax")
+    return idx, val

@@ -1,0 +1,121 @@
+"""GPU parity for the rocFFT leg of the ZC frequency-domain metric (csrc/zc_rocfft.hip,
+ofs_zc_freq_metric_fft) and the per-stream first-argmax kernel (ofs_row_argmax), through the
+C ABI: against the reference goldens (zc_freq.py:62-99 with N_FFT overridden), the CPU oracle,
+numpy's argmax (zc_freq.py:144) and the fused window-FFT kernel of ofs_zc_freq_metric.
+
+Tolerances (written here): complex128 input (rocFFT double + fp64 gather): 1e-9 relative +
+1e-11 absolute (pocketfft vs rocFFT summation order); complex64 input (rocFFT single, fp64
+gather): the metric, a ratio in [0, 1], within 2e-5 absolute.  Argmax indices exact on fp64.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import ofdm_oracle as O
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from ofdm_sync_amd import _lib, zc_freq  # noqa: E402
+
+
+def G(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def rng_c(rng, *shape):
+    return rng.standard_normal(shape) + 1j * rng.standard_normal(shape)
+
+
+@pytest.mark.parametrize("name", ["zcfreq_N2048", "zcfreq_N256"])
+def test_rocfft_vs_reference_golden(name):
+    d = G(name)
+    N, cp = int(d["N"]), int(d["CP"])
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    x = np.asarray(d["x"])
+    x = x[None] if x.ndim == 1 else x                 # (branches, T) -> one stream
+    m, pk, pv = zc_freq.compute_frequency_metric_rocfft_batched(torch.from_numpy(x[None].astype(np.complex128)).cuda(),
+                                                                idx, t, e, N=N, cp=cp, return_peak=True)
+    assert m.dtype == torch.float64 and m.shape == (1,) + d["metric"].shape
+    np.testing.assert_allclose(m[0].cpu().numpy(), d["metric"], rtol=1e-9, atol=1e-11)
+    assert int(pk[0]) == int(np.argmax(d["metric"]))
+    assert float(pv[0]) == pytest.approx(float(np.max(d["metric"])), rel=1e-9)
+
+
+@pytest.mark.parametrize("N,cp,T,nb", [(256, 64, 400, 1), (256, 64, 420, 2), (128, 0, 200, 3), (64, 16, 80, 1)])
+def test_rocfft_fp64_vs_oracle(N, cp, T, nb):
+    rng = np.random.default_rng(N * 3 + nb)
+    B = 5
+    x = rng_c(rng, B, nb, T)
+    idx, t, e = O.zc_template()
+    if T >= 40 + N:
+        x[2, :, 40:40 + N] += 4 * O.pss_symbol(N)
+    m, pk, _ = zc_freq.compute_frequency_metric_rocfft_batched(torch.from_numpy(x).cuda(), idx, t, e, N=N, cp=cp,
+                                                               return_peak=True)
+    mm = m.cpu().numpy()
+    for b in range(B):
+        mo = O.zc_freq_metric(x[b], N, cp, idx, t, e)
+        np.testing.assert_allclose(mm[b], mo, rtol=1e-9, atol=1e-11)
+        assert int(pk[b]) == int(np.argmax(mm[b]))
+
+
+@pytest.mark.parametrize("B,nb,cp,T", [(1000, 1, 0, 4096), (64, 2, 512, 4610)])
+def test_rocfft_fp32_cfg5_shape_vs_oracle_and_fused(B, nb, cp, T):
+    """cfg5 shape (N = 4096, complex64): rocFFT leg vs oracle, and vs the fused window-FFT kernel."""
+    N = 4096
+    rng = np.random.default_rng(B + nb)
+    x = rng_c(rng, B, nb, T)
+    sym = O.pss_symbol(N)
+    for b in range(0, B, 4):
+        x[b, :, cp:cp + N] += rng.uniform(0.5, 8.0) * sym
+    x = x.astype(np.complex64)
+    idx, t, e = O.zc_template()
+    xd = torch.from_numpy(x).cuda()
+    m = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp)
+    assert m.dtype == torch.float32
+    mf = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp)
+    mm = m.cpu().numpy()
+    np.testing.assert_allclose(mm, mf.cpu().numpy(), rtol=0, atol=2e-5)
+    for b in list(range(0, B, max(1, B // 16))):
+        mo = O.zc_freq_metric(x[b].astype(np.complex128), N, cp, idx, t, e)
+        np.testing.assert_allclose(mm[b], mo, rtol=0, atol=2e-5)
+    assert mm.max() > 0.5
+
+
+def test_rocfft_too_short_and_bad_input():
+    idx, t, e = O.zc_template()
+    with pytest.raises(ValueError):
+        zc_freq.compute_frequency_metric_rocfft_batched(torch.ones((2, 79), dtype=torch.complex64).cuda(),
+                                                        idx, t, e, N=64, cp=16)
+    m = zc_freq.compute_frequency_metric_rocfft_batched(torch.ones((2, 80), dtype=torch.complex64).cuda(),
+                                                        idx, t, e, N=64, cp=16)
+    assert m.shape == (2, 1)
+    with pytest.raises(ValueError):
+        zc_freq.compute_frequency_metric_rocfft_batched(torch.ones((2, 80, 2), dtype=torch.int16).cuda(),
+                                                        idx, t, e, N=64, cp=16)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_row_argmax_numpy_semantics(dtype):
+    rng = np.random.default_rng(7)
+    v = rng.integers(0, 5, size=(37, 1000)).astype(np.float64)    # many ties: first index must win
+    v[3, :] = -np.inf
+    v[4, 500] = np.nan
+    v[4, 900] = np.nan
+    v[5, 999] = 100.0
+    v[6, 0] = 100.0
+    v[7, :] = 1.0
+    idx, val = zc_freq.peak_index_batched(torch.from_numpy(v).to(dtype).cuda())
+    ref = np.argmax(v, axis=1)
+    assert np.array_equal(idx.cpu().numpy(), ref)
+    vv = val.cpu().numpy()
+    for b in range(v.shape[0]):
+        if not np.isnan(v[b, ref[b]]):
+            assert vv[b] == v[b, ref[b]]
+    idx1, _ = zc_freq.peak_index_batched(torch.tensor([[2.0]], dtype=dtype).cuda())
+    assert int(idx1[0]) == 0

@@ -264,7 +264,56 @@ def cfg3_fp64(dev, st, steps, warmup):
                 bytes_per_sample="16 in + P 16 + R 8 + M 8")
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "backend": backend}
+def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20):
+    """cfg5 through the rocFFT leg (ofs_zc_freq_metric_fft: batched rocFFT of every window into a
+    dense spectrum, then the HIP gather/metric kernel and the per-sequence argmax), same input as
+    cfg5.  alg_bytes counts the same 8 B/sample + output as cfg5 so Msamples/s and frac compare
+    directly; the path itself also writes and re-reads the spectrum (traffic_bytes)."""
+    N = 4096
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.empty((n_seq, N), dtype=torch.complex64, device=dev)
+    for i in range(0, n_seq, 1 << 17):
+        x[i:i + (1 << 17)].copy_(torch.randn((min(1 << 17, n_seq - i), N), dtype=torch.complex64, device=dev,
+                                             generator=g))
+    spec = torch.empty((n_seq, N), dtype=torch.complex64, device=dev)
+    out = torch.empty((n_seq, 1), dtype=torch.float32, device=dev)
+    pk = torch.empty((n_seq,), dtype=torch.int64, device=dev)
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    idx32 = np.ascontiguousarray(idx.astype(np.int32))
+    tb = np.ascontiguousarray(t.astype(np.complex128))
+    plan = zc_freq.FFTPlan(_lib.FP32, N, n_seq, N)
+    work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
+    L_ = _lib.lib()
+    args = (plan.handle, _lib.C64, x.data_ptr(), n_seq, 1, N, N, 0, 62, idx32.ctypes.data, tb.ctypes.data, e,
+            spec.data_ptr(), _lib.ptr(work), out.data_ptr(), pk.data_ptr(), None, st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_zc_freq_metric_fft(*args), "zc_freq rocfft"), steps, warmup, st)
+    return dict(config="cfg5_rocfft", workload=f"zc_freq 62-bin metric via rocFFT, N={N}, cp=0, {n_seq} sequences x {N} c64",
+                kernel="rocFFT fp32 C2C (batched, out-of-place) + zc_gather_kernel + row_argmax_kernel",
+                samples=n_seq * N, ms=ms, alg_bytes=n_seq * (N * 8 + 4),
+                traffic_bytes=n_seq * (2 * N * 8 + 62 * 8 + 4 + 8),
+                bytes_per_sample="8 in + 4 B per sequence out (as cfg5); spectrum write + gather on top")
+
+
+def cfg3_detect(dev, st, steps, warmup):
+    """cfg3 detect-only: the headline kernel with P/R/M not stored (null outputs),
+    events (gate, peak, P at peak, CFO, frame start) only: 8 B/sample + 4 B/stream + 64 B/event."""
+    B, T, L, E = 65536, 1024, 512, 4
+    x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, None, None, None, None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa detect-only"), steps, warmup, st)
+    stored = int(torch.clamp(n_ev, max=E).sum().item())
+    return dict(config="cfg3_detect", workload=f"sync_aa S&C fp32 detect-only, L={L}, {B} x {T} c64 (events only)",
+                kernel="aa_fast_kernel<E=2,MR=4> with P/R/M stores off", samples=B * T, ms=ms,
+                alg_bytes=B * T * 8 + B * 4 + stored * 64,
+                bytes_per_sample="8 in + 4 B/stream + 64 B/event", events_per_stream=round(stored / B, 3))
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "backend": backend}
 
 
 def main():
