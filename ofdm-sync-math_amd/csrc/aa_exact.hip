@@ -25,6 +25,10 @@ using namespace ofs;
 namespace {
 
 constexpr int XW = 256;                 // 4 waves = 4 streams per workgroup
+#ifndef OFS_XA_WG
+#define OFS_XA_WG 256
+#endif
+constexpr int XA = OFS_XA_WG;           // aa_exact_kernel workgroup (tuning builds: 64)
 
 // E consecutive int16 I/Q words (packed (I, Q) in one int32) of one lane, zero past T
 template <int E>
@@ -70,13 +74,13 @@ struct RowPrefix {
 // valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
 // ------------------------------------------------------------------------------------------
 template <int E, int MR, int NA>
-__global__ __launch_bounds__(XW) void aa_exact_kernel(AaFastArgs a) {
+__global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;
     constexpr int L = MR * RL;
     constexpr int PD = E <= 2 ? 4 : 2;                       // rows in flight ahead of use
     constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * (XW / 64) + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)blockIdx.x * (XA / 64) + (threadIdx.x >> 6);
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int nrows = (int)((T + RL - 1) / RL);
@@ -533,7 +537,7 @@ bool exact_enabled() {                  // OFS_EXACT=0 forces the general engine
 
 template <int E, int MR, int NA>
 int aa_launch(const AaFastArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((aa_exact_kernel<E, MR, NA>), dim3((unsigned)((a.B + 3) / 4)), dim3(XW), 0, st, a);
+    hipLaunchKernelGGL((aa_exact_kernel<E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 template <int E, int MR>

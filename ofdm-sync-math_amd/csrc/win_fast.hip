@@ -26,7 +26,10 @@ using namespace ofs;
 
 namespace {
 
-constexpr int WF_WG = 256;            // 4 waves = 4 streams per workgroup
+#ifndef OFS_WF_WG
+#define OFS_WF_WG 256
+#endif
+constexpr int WF_WG = OFS_WF_WG;       // 4 waves = 4 streams per workgroup (tuning builds: 64)
 enum { WF_SC = 1, WF_COMB = 2, WF_MINN = 3 };
 
 template <int MODE, int E, int MW, int NB>
@@ -385,7 +388,7 @@ __global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
 
 template <int MODE, int E, int MW, int NB>
 int launch(const WinFastArgs& a, hipStream_t st) {
-    const int64_t grid = (a.B + 3) / 4;
+    const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
     hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
@@ -425,7 +428,7 @@ void pick(int W, int& E, int& mw) {
 
 template <int E, int MW, int NB>
 int launch_fused(const WinFusedArgs& a, hipStream_t st) {
-    const int64_t grid = (a.B + 3) / 4;
+    const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
     hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--L", type=int, default=512)
     ap.add_argument("--realloc", type=int, default=0, help="only the full case, re-allocating all buffers N times")
     ap.add_argument("--same", action="store_true", help="realloc sweep without re-allocating (time variation)")
+    ap.add_argument("--contig", action="store_true", help="arena rounds use a physically contiguous arena (bench.py)")
     ap.add_argument("--pre", type=float, default=0.0, help="GiB allocated (and held) before the first round")
     ap.add_argument("--libs", default="", help="comma list of library paths timed on the same buffers (realloc)")
     a = ap.parse_args()
@@ -89,7 +90,8 @@ def realloc_sweep(a):
         else:
             if r % 2 == 1:                       # odd rounds: one arena (bench.py layout)
                 x, P, R, M = _lib.arena(dev, [((B, 1, T), torch.complex64), ((B, T), torch.complex64),
-                                              ((B, T), torch.float32), ((B, T), torch.float32)])
+                                              ((B, T), torch.float32), ((B, T), torch.float32)],
+                                             contiguous=a.contig)
                 x.copy_(synth.make_aa_batch(B, T, L, seed=2026, device=dev))
             else:
                 x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)

@@ -7,7 +7,7 @@ VARIANTS=${VARIANTS:-"w0= w4=-DOFS_FAST_WAVES=4 w5=-DOFS_FAST_WAVES=5"}
 for V in $VARIANTS; do
   NAME=${V%%=*}; FLAGS=${V#*=}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude $FLAGS \
-     -o build/libofdmsync_$NAME.so ofdm-sync-math_amd/csrc/*.hip &
+     -o build/libofdmsync_$NAME.so ofdm-sync-math_amd/csrc/*.hip -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib &
 done
 wait
 ls -la build/
