@@ -75,7 +75,24 @@ def cpu_baseline(x_dev: torch.Tensor, L: int, threads: int, gpu_M: torch.Tensor)
                 sample=f"full per-GPU batch x{reps}: {B} streams x {T} c64 (same synthetic input), "
                        f"L={L}, C restatement of sync_aa.aa_detect_streaming with OpenMP over "
                        f"streams, {threads} threads of {cores} host CPUs, {dt:.2f} s wall",
-                max_abs_err_M_vs_gpu=err)
+                max_abs_err_M_vs_gpu=err, numpy=numpy_baseline(xh, L))
+
+
+def numpy_baseline(xh: np.ndarray, L: int, budget_s: float = 3.0):
+    """The NumPy restatement of the path (oracle/ofdm_oracle.aa_detect: vectorised prefix sums +
+    the reference's gate loop), one process, streams of the same batch one after another until
+    ~budget_s of wall time: the north star's "NumPy CPU path" beside the C port."""
+    import ofdm_oracle
+    B, _, T = xh.shape
+    ofdm_oracle.aa_detect(xh[0].astype(np.complex128), L)                 # warm
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s and n < B:
+        ofdm_oracle.aa_detect(xh[n].astype(np.complex128), L)
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n * T / dt / 1e6, unit="Msamples/s", cores=1, kind="port",
+                sample=f"{n} streams x {T} c64 of the same batch, L={L}, NumPy restatement "
+                       f"(ofdm_oracle.aa_detect, fp64), one process, {dt:.2f} s wall")
 
 
 def kernel_label(plan: int) -> str:

@@ -76,6 +76,8 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
  *                      L = 64*E*MR), complex64 / OFS_FP32 / 1-2 antennas / even T <= 1024;
  *   2000 + 10*E + MR : integer-exact wave-per-stream path, OFS_CI16 / OFS_FP64, 1-2 antennas,
  *                      T * n_ant <= 2^21 (all window sums exact integers), L = 64*E*MR, MR <= 8;
+ *   3000 + 10*E + MR : the same wave-per-stream kernel on OFS_C128 / OFS_FP64 input (fp64 prefix
+ *                      differences over the stream, T <= 3584 = the general engine's fp64 tile);
  *   1                : general LDS engine, events fused (stream fits one tile);
  *   2                : general LDS engine, tiled, events in a second pass over P/M;
  *   <0               : invalid arguments or window too long (as ofs_aa_detect would return).

@@ -54,6 +54,31 @@ __device__ __forceinline__ void load_words(const int32_t* xs, int64_t n0, int64_
 __device__ __forceinline__ double w_re(int32_t w) { return (double)(int16_t)(w & 0xffff); }
 __device__ __forceinline__ double w_im(int32_t w) { return (double)(w >> 16); }
 
+// sample access of the wave-per-stream sync_aa kernel: int16 I/Q words (exact integer sums) or
+// complex128 (fp64 prefix differences over the stream, the general engine's arithmetic)
+template <int FMT> struct XSamp;
+template <> struct XSamp<OFS_CI16> {
+    using W = int32_t;
+    static __device__ __forceinline__ W zero() { return 0; }
+    static __device__ __forceinline__ double re(W w) { return w_re(w); }
+    static __device__ __forceinline__ double im(W w) { return w_im(w); }
+    template <int E>
+    static __device__ __forceinline__ void load(const W* xs, int64_t n0, int64_t T, W (&w)[E]) {
+        load_words<E>(xs, n0, T, w);
+    }
+};
+template <> struct XSamp<OFS_C128> {
+    using W = double2;
+    static __device__ __forceinline__ W zero() { return make_double2(0.0, 0.0); }
+    static __device__ __forceinline__ double re(W w) { return w.x; }
+    static __device__ __forceinline__ double im(W w) { return w.y; }
+    template <int E>
+    static __device__ __forceinline__ void load(const W* xs, int64_t n0, int64_t T, W (&w)[E]) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) w[e] = (n0 + e < T) ? xs[n0 + e] : zero();
+    }
+};
+
 // in-lane inclusive prefix of v, then the lane's exclusive wave prefix and the row total
 template <int E>
 struct RowPrefix {
@@ -69,12 +94,15 @@ struct RowPrefix {
 };
 
 // ------------------------------------------------------------------------------------------
-// sync_aa, integer input.  P[n] = A(n) - A(n-L), R[n] = Ae(n) - Ae(n-L) with A the prefix of
+// sync_aa, integer input (FMT = OFS_CI16, exact) or complex128 (OFS_C128, T <= 3584: the same
+// stream-wide fp64 prefix span as the general engine's tiles).  P[n] = A(n) - A(n-L), R[n] = Ae(n) - Ae(n-L) with A the prefix of
 // x[j]·conj(x[j-L]) (0 while the delay line fills) and Ae that of |x[j]|², summed over antennas;
 // valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
 // ------------------------------------------------------------------------------------------
-template <int E, int MR, int NA>
+template <int FMT, int E, int MR, int NA>
 __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
+    using X = XSamp<FMT>;
+    using W = typename X::W;
     constexpr int RL = 64 * E;
     constexpr int L = MR * RL;
     constexpr int PD = E <= 2 ? 4 : 2;                       // rows in flight ahead of use
@@ -84,9 +112,9 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int nrows = (int)((T + RL - 1) / RL);
-    const int32_t* xs = reinterpret_cast<const int32_t*>(a.x) + b * NA * T;
+    const W* xs = reinterpret_cast<const W*>(a.x) + b * NA * T;
 
-    int32_t lag[NA][MR][E];                                  // raw words of rows k-MR..k-1
+    W lag[NA][MR][E];                                        // raw samples of rows k-MR..k-1
     double Ar[MR][E], Ai[MR][E], Ae[MR][E];                  // prefix values of rows k-MR..k-1
 #pragma unroll
     for (int m = 0; m < MR; ++m)
@@ -94,15 +122,15 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
         for (int e = 0; e < E; ++e) {
             Ar[m][e] = 0.0; Ai[m][e] = 0.0; Ae[m][e] = 0.0;
 #pragma unroll
-            for (int t = 0; t < NA; ++t) lag[t][m][e] = 0;
+            for (int t = 0; t < NA; ++t) lag[t][m][e] = X::zero();
         }
     double CR = 0.0, CI = 0.0, CE = 0.0;                     // prefix at the start of row k
 
-    int32_t nx[PD][NA][E];
+    W nx[PD][NA][E];
 #pragma unroll
     for (int p = 0; p < PD; ++p)
 #pragma unroll
-        for (int t = 0; t < NA; ++t) load_words<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
+        for (int t = 0; t < NA; ++t) X::template load<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
 
     AaRowGate<E, double> gate;
     if (a.detect)
@@ -120,7 +148,7 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
             const int k = k0 + u;
             if (k < nrows) {
                 const int nb = RL * k + E * lane;
-                int32_t cur[NA][E];
+                W cur[NA][E];
 #pragma unroll
                 for (int t = 0; t < NA; ++t)
 #pragma unroll
@@ -128,7 +156,7 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
                 if (k + PD < nrows) {
 #pragma unroll
                     for (int t = 0; t < NA; ++t)
-                        load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[u % PD][t]);
+                        X::template load<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[u % PD][t]);
                 }
                 const int sl = u % MR;                       // ring slot of row k-MR (and k)
                 double pr[E], pi[E], en[E];
@@ -137,8 +165,8 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
                     pr[e] = 0.0; pi[e] = 0.0; en[e] = 0.0;
 #pragma unroll
                     for (int t = 0; t < NA; ++t) {
-                        const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
-                        const double dr = w_re(lag[t][sl][e]), di = w_im(lag[t][sl][e]);
+                        const double xr = X::re(cur[t][e]), xi = X::im(cur[t][e]);
+                        const double dr = X::re(lag[t][sl][e]), di = X::im(lag[t][sl][e]);
                         pr[e] += xr * dr + xi * di;                  // x[n]·conj(x[n-L]), exact
                         pi[e] += xi * dr - xr * di;
                         en[e] += xr * xr + xi * xi;
@@ -536,25 +564,28 @@ bool exact_enabled() {                  // OFS_EXACT=0 forces the general engine
 }
 
 template <int E, int MR, int NA>
-int aa_launch(const AaFastArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((aa_exact_kernel<E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+int aa_launch(int fmt, const AaFastArgs& a, hipStream_t st) {
+    if (fmt == OFS_C128)
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+    else
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 template <int E, int MR>
-int aa_launch_na(int na, const AaFastArgs& a, hipStream_t st) {
+int aa_launch_na(int fmt, int na, const AaFastArgs& a, hipStream_t st) {
     switch (na) {
-        case 1: return aa_launch<E, MR, 1>(a, st);
-        case 2: return aa_launch<E, MR, 2>(a, st);
+        case 1: return aa_launch<E, MR, 1>(fmt, a, st);
+        case 2: return aa_launch<E, MR, 2>(fmt, a, st);
     }
     return 0;
 }
 template <int E>
-int aa_launch_mr(int mr, int na, const AaFastArgs& a, hipStream_t st) {
+int aa_launch_mr(int fmt, int mr, int na, const AaFastArgs& a, hipStream_t st) {
     switch (mr) {
-        case 1: return aa_launch_na<E, 1>(na, a, st);
-        case 2: return aa_launch_na<E, 2>(na, a, st);
-        case 4: return aa_launch_na<E, 4>(na, a, st);
-        case 8: return aa_launch_na<E, 8>(na, a, st);
+        case 1: return aa_launch_na<E, 1>(fmt, na, a, st);
+        case 2: return aa_launch_na<E, 2>(fmt, na, a, st);
+        case 4: return aa_launch_na<E, 4>(fmt, na, a, st);
+        case 8: return aa_launch_na<E, 8>(fmt, na, a, st);
     }
     return 0;
 }
@@ -577,21 +608,25 @@ int rtl_launch(const RtlExactArgs& a, hipStream_t st) {
 
 }  // namespace
 
-// 10*E + MR of the exact aa kernel for a shape, 0 if not covered
+// 10*E + MR of the wave-per-stream fp64 aa kernel for a shape (+100 for complex128 input), 0 if
+// not covered
 int ofs_aa_exact_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
-    if (fmt != OFS_CI16 || precision != OFS_FP64 || n_ant < 1 || n_ant > 2 || !exact_enabled()) return 0;
-    if (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2) return 0;   // sums < 2^53
-    if (L == 64) return 11;
-    if (L % 128 == 0 && (L == 128 || L == 256 || L == 512 || L == 1024)) return 20 + L / 128;
+    if ((fmt != OFS_CI16 && fmt != OFS_C128) || precision != OFS_FP64 || n_ant < 1 || n_ant > 2 || !exact_enabled())
+        return 0;
+    if (fmt == OFS_CI16 && (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2)) return 0;   // sums < 2^53
+    if (fmt == OFS_C128 && (T < 1 || T > 3584)) return 0;    // the general engine's fp64 tile span
+    const int f = fmt == OFS_C128 ? 100 : 0;
+    if (L == 64) return f + 11;
+    if (L % 128 == 0 && (L == 128 || L == 256 || L == 512 || L == 1024)) return f + 20 + L / 128;
     return 0;
 }
 
 int ofs_aa_exact_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
     const int plan = ofs_aa_exact_plan(fmt, precision, n_ant, a.T, a.L);
     if (!plan) return 0;
-    const int E = plan / 10, mr = plan % 10;
-    if (E == 1) return aa_launch_na<1, 1>(n_ant, a, st);
-    return aa_launch_mr<2>(mr, n_ant, a, st);
+    const int E = (plan % 100) / 10, mr = plan % 10;
+    if (E == 1) return aa_launch_na<1, 1>(fmt, n_ant, a, st);
+    return aa_launch_mr<2>(fmt, mr, n_ant, a, st);
 }
 
 int ofs_rtl_exact_plan(int fmt, int n_br, int64_t T, int Q) {

@@ -878,7 +878,7 @@ int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T,
     const int fp = ofs_aa_fast_plan(in_fmt, precision, n_ant, T, L);
     if (fp) return 1000 + fp;
     const int xp = ofs_aa_exact_plan(in_fmt, precision, n_ant, T, L);
-    if (xp) return 2000 + xp;
+    if (xp) return (xp >= 100 ? 3000 : 2000) + xp % 100;
     if (2 * (int64_t)L - 1 > 0x3fffffff) return OFS_ETOOLONG;
     Plan p;
     const int lo = -(int)(2 * (int64_t)L - 1);

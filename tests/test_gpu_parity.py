@@ -462,7 +462,8 @@ def test_aa_fast_path_sweep(L, T):
 
 def test_aa_fast_path_is_used_for_the_benchmark_shape():
     assert _lib.lib().ofs_aa_plan(_lib.C64, _lib.FP32, 1, 1024, 512) >= 1000
-    assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, 1, 1024, 512) in (1, 2)
+    assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, 1, 1024, 512) == 3024      # fp64 wave-per-stream
+    assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, 1, 9000, 512) in (1, 2)    # general engine
 
 
 # ------------------------------------------------------ receiver back-end ------------
