@@ -216,8 +216,18 @@ struct WinFusedArgs {
     float* Ms; float2* Ps; float* Rs; float* Mm; float2* Pm; float* Rm;
 };
 
+// occupancy bound (min waves per SIMD) of the fused kernel; tuning builds set -DOFS_SCM_WAVES=N
+#ifndef OFS_SCM_WAVES
+#define OFS_SCM_WAVES 0
+#endif
+#if OFS_SCM_WAVES > 0
+#define OFS_SCM_BOUNDS __launch_bounds__(WF_WG, OFS_SCM_WAVES)
+#else
+#define OFS_SCM_BOUNDS __launch_bounds__(WF_WG)
+#endif
+
 template <int E, int MW, int NB>
-__global__ __launch_bounds__(WF_WG) void sc_minn_fast_kernel(WinFusedArgs a) {
+__global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     constexpr int RL = 64 * E;
     constexpr int N = 4 * MW * RL;
     constexpr int XR = 2 * MW;                  // x ring / S_h suffix ring / S_q history ring
