@@ -313,7 +313,38 @@ def cfg3_detect(dev, st, steps, warmup):
                 bytes_per_sample="8 in + 4 B/stream + 64 B/event", events_per_stream=round(stored / B, 3))
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "backend": backend}
+def cfg3_pcie(dev, st, steps, warmup):
+    """cfg3 with the batch handed over in host memory (the numpy drop-in's situation): pinned host
+    x -> HBM, the headline kernel, P/R/M back to pinned host, all on one stream.  The PCIe-inclusive
+    rate DESIGN.md quotes beside the HBM-resident headline; never the bench value."""
+    B, T, L, E = 65536, 1024, 512, 4
+    xh = synth.make_aa_batch(B, T, L, seed=2026, device=dev).cpu().pin_memory()
+    x = torch.empty((B, 1, T), dtype=torch.complex64, device=dev)
+    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
+    R = torch.empty((B, T), dtype=torch.float32, device=dev)
+    M = torch.empty_like(R)
+    Ph, Rh, Mh = (torch.empty(t.shape, dtype=t.dtype).pin_memory() for t in (P, R, M))
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+
+    def step():
+        x.copy_(xh, non_blocking=True)
+        chk(L_.ofs_aa_detect(*args), "aa")
+        Ph.copy_(P, non_blocking=True)
+        Rh.copy_(R, non_blocking=True)
+        Mh.copy_(M, non_blocking=True)
+
+    ms = timed(step, steps, warmup, st)
+    return dict(config="cfg3_pcie", workload=f"cfg3 with host-resident input/outputs (pinned), {B} x {T} c64",
+                kernel="H2D copy + aa_fast_kernel + 3 x D2H copy (one stream)", samples=B * T, ms=ms,
+                alg_bytes=B * T * 24, bytes_per_sample="8 H2D + 16 D2H (PCIe) per sample")
+
+
+CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
 def main():
