@@ -100,7 +100,7 @@ struct RowPrefix {
 // valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
 // ------------------------------------------------------------------------------------------
 template <int FMT, int E, int MR, int NA>
-__global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
+__global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1) void aa_exact_kernel(AaFastArgs a) {
     using X = XSamp<FMT>;
     using W = typename X::W;
     constexpr int RL = 64 * E;
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(XA) void aa_exact_kernel(AaFastArgs a) {
 #pragma unroll
         for (int t = 0; t < NA; ++t) X::template load<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
 
-    AaRowGate<E, double> gate;
+    AaRowGate<E, double, false, true, FMT != OFS_C128> gate;
     if (a.detect)
         gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
                   a.ev_r + b * (int64_t)a.max_ev * 4);
@@ -615,6 +615,7 @@ int ofs_aa_exact_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
         return 0;
     if (fmt == OFS_CI16 && (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2)) return 0;   // sums < 2^53
     if (fmt == OFS_C128 && (T < 1 || T > 3584)) return 0;    // the general engine's fp64 tile span
+    if (fmt == OFS_C128 && n_ant == 2 && L > 512) return 0;  // fp64 rings of 2 x 1024 lags spill
     const int f = fmt == OFS_C128 ? 100 : 0;
     if (L == 64) return f + 11;
     if (L % 128 == 0 && (L == 128 || L == 256 || L == 512 || L == 1024)) return f + 20 + L / 128;

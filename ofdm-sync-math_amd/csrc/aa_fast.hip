@@ -77,7 +77,8 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 // ds_read_b128.  Paired A/B on the same buffers: registers 1-3 % faster (profiles/
 // r01c_staging_ab.log; the SOL probe shows the same 8 % gap between LDS-DMA and register staging
 // of this read/write pattern).
-template <int E, int MR, int NA>
+// DO: detect-only instantiation (P/R/M/valid not stored, events only: SURVEY §8d)
+template <int E, int MR, int NA, bool DO>
 __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;                 // samples per row
     constexpr int RW = TMAX / RL;              // rows per stream
@@ -140,14 +141,14 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     double Cr[RW + 1], Ci[RW + 1], Ce[RW + 1];  // running row bases (wave-uniform)
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
-    AaRowGate<E, float> gate;                   // event state (wave-uniform)
+    AaRowGate<E, float, false, DO> gate;        // event state (wave-uniform)
     if (a.detect)
         gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
                   a.ev_r + b * (int64_t)a.max_ev * 4);
 
-    float* Pout = reinterpret_cast<float*>(a.P);
-    float* Rout = reinterpret_cast<float*>(a.R);
-    float* Mout = reinterpret_cast<float*>(a.M);
+    float* Pout = DO ? nullptr : reinterpret_cast<float*>(a.P);
+    float* Rout = DO ? nullptr : reinterpret_cast<float*>(a.R);
+    float* Mout = DO ? nullptr : reinterpret_cast<float*>(a.M);
     const float floor_ = 1e-6f * (float)L;
 
 #pragma unroll
@@ -228,7 +229,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
                         if (Mout) st_out(reinterpret_cast<float4*>(Mout + o + 2 * j),
                                         make_float4(mf[2 * j], mf[2 * j + 1], mf[2 * j + 2], mf[2 * j + 3]));
                     }
-                    if (a.valid) { a.valid[o + 2 * j] = (k >= MR); a.valid[o + 2 * j + 1] = (k >= MR); }
+                    if (!DO && a.valid) { a.valid[o + 2 * j] = (k >= MR); a.valid[o + 2 * j + 1] = (k >= MR); }
                 }
             }
 
@@ -246,8 +247,12 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 
 template <int E, int MR, int NA>
 int launch(const AaFastArgs& a, hipStream_t st) {
+    const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
     const int64_t grid = (a.B + FAST_WG / 64 - 1) / (FAST_WG / 64);
-    hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
+    if (det_only)
+        hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
+    else
+        hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 

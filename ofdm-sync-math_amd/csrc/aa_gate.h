@@ -12,16 +12,30 @@
 // <= n, a gate closes at n iff prev(n) exists and n - prev(n) == max(H, 1); it opens at an above
 // sample whose predecessor gap is >= max(H, 1); opens and closes alternate; the peak is the
 // arg-extremum over [open, close].  Rows hold RL = 64·E samples, lane l owns samples
-// RL·k + E·l + e.  Per row: prev-above by lane-serial + DPP max-scan, opens / closes by ballot,
-// per-gate arg-extremum by wave max/min reductions; state carried between rows in scalars.
+// RL·k + E·l + e.  Per row: prev-above by lane-serial + DPP max-scan, opens / closes by ballot
+// (with H >= RL: from the row's first/last above bits alone, no scan); the per-gate
+// arg-extremum is tracked per lane across rows and reduced over the wave once per event.
 #pragma once
 #include "ofs_common.h"
 
 namespace ofs {
 
-constexpr int GATE_NOKEY = 1 << 20;
+// gate machine variants (paired A/B builds): scan-free flags when H >= RL (template FF: on for
+// the fp64 kernels and the detect-only fp32 kernel - 5-8 % there - off for the fp32 kernel that
+// also stores P/R/M, where it measured 1-2 % slower); per-lane peak tracking reduced over the
+// wave once per event instead of once per row (template DEFER; neutral on the headline, off
+// for the complex128 kernel whose extra fp64 lane state cost it occupancy)
+#ifndef OFS_GATE_FASTFLAGS
+#define OFS_GATE_FASTFLAGS 1
+#endif
+#ifndef OFS_GATE_DEFER
+#define OFS_GATE_DEFER 1
+#endif
 
-template <int E, class V, bool RTL = false>
+constexpr int GATE_NOKEY = 1 << 20;      // row-relative keys
+constexpr int ABS_NOKEY = 0x7fffffff;    // absolute sample indices
+
+template <int E, class V, bool RTL = false, bool FF = true, bool DEFER = true>
 struct AaRowGate {
     static constexpr int RL = 64 * E;
     int Hp, L, max_ev, toff;
@@ -37,6 +51,7 @@ struct AaRowGate {
         L = L_; max_ev = max_ev_; thr = thr_; fs = fs_; evi = evi_; evr = evr_; toff = toff_;
         carry_last = -1; n_ev = 0; ev_start = 0; gate_open = 0; bidx = 0;
         bpm = (V)-1; bpr = (V)0; bpi = (V)0; bm = (V)0;
+        lane_reset();
     }
 
     // the record is wave-uniform: lanes 0..3 store the four int64 fields and lanes 4..7 the four
@@ -75,10 +90,90 @@ struct AaRowGate {
         row_flags(lane, k, nb, T, ab, pm, pr, pi, m);
     }
 
+    // per-lane running arg-extremum of the open gate: each lane keeps its best (value, absolute
+    // index, payload) over the rows the gate has covered; the wave reduction runs once, when the
+    // gate closes (first max / strict > for sync_aa, last max / >= for minn_rtl, as a global scan)
+    V lv, lpr, lpi, lm;
+    int lk;
+    __device__ __forceinline__ void lane_reset() {
+        lv = (V)-1; lpr = (V)0; lpi = (V)0; lm = (V)0;
+        lk = RTL ? -1 : ABS_NOKEY;
+    }
+    __device__ __forceinline__ void accumulate(int lane, int k, int nb, int T, int lo, int hi, const V (&pm)[E],
+                                               const V (&pr)[E], const V (&pi)[E], const V (&m)[E]) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int key = E * lane + e;
+            const bool in = nb + e < T && key >= lo && key <= hi;
+            const bool better = RTL ? (pm[e] >= lv) : (pm[e] > lv);
+            if (in && better) { lv = pm[e]; lk = RL * k + key; lpr = pr[e]; lpi = pi[e]; lm = m[e]; }
+        }
+    }
+    // wave reduction of the lanes' running bests into the event's peak (kept if it beats the
+    // peak so far under the machine's tie rule), then the lanes restart
+    __device__ __forceinline__ void merge() {
+        const V vmax = wave_max(lv);
+        const int kk = RTL ? wave_max_i(lv == vmax ? lk : -1) : wave_min(lv == vmax ? lk : ABS_NOKEY);
+        const bool found = RTL ? (kk >= 0) : (kk != ABS_NOKEY);
+        const bool take = RTL ? (vmax >= bpm) : (vmax > bpm);
+        if (found && take) {
+            const int ln = (kk % RL) / E;
+            bpr = readlane(lpr, ln);
+            bpi = readlane(lpi, ln);
+            bm = readlane(lm, ln);
+            bpm = vmax;
+            bidx = kk;
+        }
+        lane_reset();
+    }
+    // a gate's samples within one row; OFS_GATE_DEFER = 0 reduces over the wave every row
+    __device__ __forceinline__ void seg(int lane, int k, int nb, int T, int lo, int hi, const V (&pm)[E],
+                                        const V (&pr)[E], const V (&pi)[E], const V (&m)[E]) {
+        accumulate(lane, k, nb, T, lo, hi, pm, pr, pi, m);
+        if (!(DEFER && OFS_GATE_DEFER)) merge();
+    }
+    __device__ __forceinline__ void open_at(int start) {
+        gate_open = 1; ev_start = start; bpm = (V)-1; lane_reset();
+    }
+
     // generic row: above flags given; pm = the value whose arg-extremum is the peak
     __device__ __forceinline__ void row_flags(int lane, int k, int nb, int T, const bool (&ab)[E],
                                               const V (&pm)[E], const V (&pr)[E], const V (&pi)[E],
                                               const V (&m)[E]) {
+        if (FF && OFS_GATE_FASTFLAGS && Hp >= RL) {
+            // hysteresis at least one row: only the row's FIRST above sample can open a gate and
+            // only carry_last + Hp can close one (before that first sample), so the machine runs
+            // on the above ballots alone, in scalar registers - no prefix scan
+            int first = GATE_NOKEY, last = -1;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t am = __ballot(ab[e]);
+                if (am) {
+                    first = min(first, E * (int)__builtin_ctzll(am) + e);
+                    last = max(last, E * (63 - (int)__builtin_clzll(am)) + e);
+                }
+            }
+            const int base = RL * k;
+            int seg_lo = gate_open ? 0 : -1;
+            if (carry_last >= 0) {                                   // close at carry_last + Hp
+                const int c = carry_last + Hp;
+                if (c >= base && c < base + RL && c < T && c - base < first) {
+                    seg(lane, k, nb, T, seg_lo, c - base, pm, pr, pi, m);
+                    if (DEFER && OFS_GATE_DEFER) merge();
+                    emit(lane, c);
+                    gate_open = 0; seg_lo = -1;
+                }
+            }
+            if (first != GATE_NOKEY) {
+                const int f = base + first;
+                if (carry_last < 0 || f - 1 - carry_last >= Hp) {   // open
+                    open_at(f); seg_lo = first;
+                }
+                carry_last = base + last;
+            }
+            if (gate_open) seg(lane, k, nb, T, seg_lo, RL - 1, pm, pr, pi, m);
+            return;
+        }
         int lane_last = -1;
 #pragma unroll
         for (int e = 0; e < E; ++e)
@@ -100,31 +195,6 @@ struct AaRowGate {
         }
         carry_last = readlane(W, 63);
 
-        // arg-extremum of pm on keys [lo, hi]: sync_aa first max (strict >), minn_rtl last max (>=)
-        auto seg_reduce = [&](int lo, int hi) {
-            V lv = (V)-1, lpr = (V)0, lpi = (V)0, lm = (V)0;
-            int lk = RTL ? -1 : GATE_NOKEY;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                const int key = E * lane + e;
-                const bool in = nb + e < T && key >= lo && key <= hi;
-                const bool better = RTL ? (pm[e] >= lv) : (pm[e] > lv);
-                if (in && better) { lv = pm[e]; lk = key; lpr = pr[e]; lpi = pi[e]; lm = m[e]; }
-            }
-            const V vmax = wave_max(lv);
-            const int kk = RTL ? wave_max_i(lv == vmax ? lk : -1) : wave_min(lv == vmax ? lk : GATE_NOKEY);
-            const bool found = RTL ? (kk >= 0) : (kk != GATE_NOKEY);
-            const bool take = RTL ? (vmax >= bpm) : (vmax > bpm);
-            if (take && found) {
-                const int ln = kk / E;
-                bpr = readlane(lpr, ln);
-                bpi = readlane(lpi, ln);
-                bm = readlane(lm, ln);
-                bpm = vmax;
-                bidx = RL * k + kk;
-            }
-        };
-
         int seg_lo = gate_open ? 0 : -1;
         if (any) {
             int pos = -1;
@@ -141,16 +211,17 @@ struct AaRowGate {
                 }
                 if (key == GATE_NOKEY) break;
                 if (is_open) {
-                    gate_open = 1; ev_start = RL * k + key; seg_lo = key; bpm = (V)-1;
+                    open_at(RL * k + key); seg_lo = key;
                 } else {
-                    seg_reduce(seg_lo, key);
+                    seg(lane, k, nb, T, seg_lo, key, pm, pr, pi, m);
+                    if (DEFER && OFS_GATE_DEFER) merge();
                     emit(lane, RL * k + key);
                     gate_open = 0; seg_lo = -1;
                 }
                 pos = key;
             }
         }
-        if (gate_open) seg_reduce(seg_lo, RL - 1);
+        if (gate_open) seg(lane, k, nb, T, seg_lo, RL - 1, pm, pr, pi, m);
     }
 
     // end of stream.  sync_aa: a gate still open closes at T (sync_aa.py:560-568);
@@ -162,7 +233,7 @@ struct AaRowGate {
                 if (open_start) *open_start = gate_open ? ev_start : -1;
             }
         } else {
-            if (gate_open) emit(lane, T);
+            if (gate_open) { if (DEFER && OFS_GATE_DEFER) merge(); emit(lane, T); }
             if (lane == 0) *n_ev_out = n_ev;
         }
     }

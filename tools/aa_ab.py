@@ -104,7 +104,7 @@ def realloc_sweep(a):
         args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
                 0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
         res = {}
-        for name, lib in libs:
+        for name, lib in libs[r % len(libs):] + libs[:r % len(libs)]:     # rotate the order per round
             for _ in range(a.warmup):
                 lib.ofs_aa_detect(*args)
             torch.cuda.synchronize()
@@ -115,6 +115,7 @@ def realloc_sweep(a):
             e1.record(st)
             torch.cuda.synchronize()
             res[name] = round(e0.elapsed_time(e1) / a.steps, 5)
+        res = {n: res[n] for n, _ in libs}
         print(json.dumps({"round": r, "ms": res, "x": hex(x.data_ptr()), "P": hex(P.data_ptr())}), flush=True)
         if not a.same or len(keep) == 0:
             keep.append((x, P, R, M))             # hold: the next round gets new physical pages
