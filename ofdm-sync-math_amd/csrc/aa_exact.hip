@@ -326,7 +326,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     double CC = 0.0, CE = 0.0;
     double sm = 0.0;                                               // IIR state carried between segments
     long long si = 0;
-    AaRowGate<SC, double, true> gate;                              // detect_minn_rtl, closed form
+    AaRowGate<SC, double, true, true, false> gate;                 // detect_minn_rtl, closed form
     if (a.detect)
         gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
                   nullptr, a.toff);
