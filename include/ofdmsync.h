@@ -10,6 +10,7 @@
  * Conventions (all entry points):
  *   - every pointer is a DEVICE pointer (hipMalloc'd / torch CUDA tensor storage),
  *     except where noted; buffers are caller-allocated, nothing is allocated inside;
+ *   - a pointer may be NULL when the buffer it describes is empty (B = 0 or T = 0);
  *   - input samples are laid out [B][n_branch][T] (stream-major, branch, time), the
  *     branch axis is SUMMED exactly like axis 0 of the reference's 2-D inputs;
  *   - outputs are laid out [B][n_out];

@@ -285,9 +285,9 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
                                   const void* data_used, int64_t data_stride, double* cfo_out, void* h_out,
                                   void* xa_out, void* gain_out, double* evm_out, double* evm_db_out,
                                   double* slope_out, double* sto_out, void* stream) {
-    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || !x || B < 0 || n_br < 1 ||
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 ||
         T < 0 || n_fft < 2 || n_fft > BNMAX || (n_fft & (n_fft - 1)) || cp_len < 0 || n_used < 1 ||
-        n_used > n_fft || !pilot_start || !data_start || !bins || !pilot_used || !data_used ||
+        n_used > n_fft || OFS_MISSING(pilot_start, B) || OFS_MISSING(data_start, B) || !bins || !pilot_used || !data_used ||
         pilot_stride < 0 || data_stride < 0 || B > 0x7fffffff)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;

@@ -909,7 +909,7 @@ extern "C" {
 
 int32_t ofs_park_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                         int32_t N, int32_t precision, void* M, void* P, void* E, void* stream) {
-    if (!fmt_ok(in_fmt) || !(precision == OFS_FP32 || precision == OFS_FP64) || !x || B < 0 ||
+    if (!fmt_ok(in_fmt) || !(precision == OFS_FP32 || precision == OFS_FP64) || OFS_MISSING(x, B * T) || B < 0 ||
         n_br < 1 || T < 0 || N < 0)
         return OFS_EINVAL;
     const int half = N / 2;
@@ -934,8 +934,9 @@ int32_t ofs_park_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, 
 int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                          const void* ref, int32_t N, double ref_energy, int32_t mode,
                          const void* corr_in, void* corr, double* corr_mag, void* stream) {
-    if (!fmt_ok(in_fmt) || !x || !ref || B < 0 || n_br < 1 || T < 1 || N < 1 || mode < 0 ||
-        mode > 4 || (!corr && !corr_mag) || (mode == 3 && (!corr_in || n_br != 1)) || ref_energy < 0)
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || !ref || B < 0 || n_br < 1 || T < 1 || N < 1 || mode < 0 ||
+        mode > 4 || (!corr && !corr_mag && B > 0) || (mode == 3 && (OFS_MISSING(corr_in, B) || n_br != 1)) ||
+        ref_energy < 0)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     ZcArgs a;
@@ -956,7 +957,7 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
                            int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
                            const int32_t* bin_indices, const double* template_bins,
                            double template_energy, void* metric, void* stream) {
-    if (!fmt_ok(in_fmt) || !x || !metric || !bin_indices || !template_bins || B < 0 || n_br < 1 ||
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || OFS_MISSING(metric, B) || !bin_indices || !template_bins || B < 0 || n_br < 1 ||
         T < 0 || N < 1 || cp < 0 || n_bins < 1 || n_bins > 64 ||
         !(precision == OFS_FP32 || precision == OFS_FP64))
         return OFS_EINVAL;

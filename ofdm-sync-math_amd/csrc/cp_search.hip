@@ -128,8 +128,8 @@ extern "C" int32_t ofs_cp_search(int32_t in_fmt, const void* x, int64_t B, int32
                                  const int64_t* est, int32_t n_fft, int32_t win_len, int32_t span,
                                  int32_t mode, double fs_hz, double* P_out, int64_t* d_out,
                                  double* cfo_out, int32_t* status, void* stream) {
-    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || !x || !est || !cfo_out ||
-        !status || B < 0 || n_br < 1 || T < 0 || n_fft < 0 || win_len < 1 || span < 0 ||
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || OFS_MISSING(x, B * T) || OFS_MISSING(est, B) ||
+        OFS_MISSING(cfo_out, B) || OFS_MISSING(status, B) || B < 0 || n_br < 1 || T < 0 || n_fft < 0 || win_len < 1 || span < 0 ||
         (mode != 0 && mode != 1) || B > 0x7fffffff)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;

@@ -824,9 +824,10 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
                       int32_t detect, double threshold, int32_t hysteresis, double sample_rate,
                       int32_t max_events, int32_t* n_events, int64_t* ev_int, double* ev_real,
                       void* stream) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || !x || B < 0 || n_ant < 1 || T < 0 || L < 1)
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_ant < 1 || T < 0 || L < 1)
         return OFS_EINVAL;
-    if (detect && (!n_events || max_events < 0 || (max_events > 0 && (!ev_int || !ev_real))))
+    if (detect && (OFS_MISSING(n_events, B) || max_events < 0 ||
+                   (max_events > 0 && B > 0 && (!ev_int || !ev_real))))
         return OFS_EINVAL;
     if (B == 0 || T == 0) return OFS_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -891,7 +892,7 @@ int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T,
 int32_t ofs_sc_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                       int32_t symbol_len, int32_t r_mode, int32_t precision,
                       void* M, void* P, void* R, void* stream) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || !x || B < 0 || n_br < 1 || T < 0)
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0)
         return OFS_EINVAL;
     if (symbol_len < 2 || (symbol_len & 1) || (r_mode != 0 && r_mode != 1)) return OFS_EINVAL;
     const int64_t n_out = T - symbol_len + 1;
@@ -912,7 +913,7 @@ int32_t ofs_sc_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, in
 int32_t ofs_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                         int32_t symbol_len, int32_t precision, void* M, void* P, void* R,
                         void* stream) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || !x || B < 0 || n_br < 1 || T < 0 || symbol_len < 1)
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0 || symbol_len < 1)
         return OFS_EINVAL;
     const int64_t n_out = T - symbol_len + 1;
     if (B == 0 || n_out <= 0) return OFS_OK;
@@ -936,11 +937,12 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
                      int32_t detect, int32_t hysteresis, int32_t timing_offset,
                      int32_t max_events, int32_t* n_events, int64_t* events,
                      int64_t* open_gate_start, void* stream) {
-    if (!fmt_ok(in_fmt) || !x || B < 0 || n_br < 1 || T < 0 || Q < 1) return OFS_EINVAL;
-    if (!corr_total || !energy_total || smooth_shift < 0 || smooth_shift > 62 ||
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0 || Q < 1) return OFS_EINVAL;
+    if (OFS_MISSING(corr_total, B * T) || OFS_MISSING(energy_total, B * T) || smooth_shift < 0 || smooth_shift > 62 ||
         threshold_frac_bits < 0 || threshold_frac_bits > 62 || (smooth_mode != 0 && smooth_mode != 1))
         return OFS_EINVAL;
-    if (detect && (!n_events || max_events < 0 || (max_events > 0 && !events))) return OFS_EINVAL;
+    if (detect && (OFS_MISSING(n_events, B) || max_events < 0 || (max_events > 0 && OFS_MISSING(events, B))))
+        return OFS_EINVAL;
     if (B == 0 || T == 0) return OFS_OK;
     if (3 * (int64_t)Q - 1 > 0x3fffffff) return OFS_ETOOLONG;
     hipStream_t st = (hipStream_t)stream;
@@ -1000,7 +1002,7 @@ int32_t ofs_minn_rtl_gate(const double* corr_positive, const uint8_t* above_thre
 int32_t ofs_sc_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                            int32_t symbol_len, int32_t precision, void* M_sc, void* P_sc, void* R_sc,
                            void* M_minn, void* P_minn, void* R_minn, void* stream) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || !x || B < 0 || n_br < 1 || T < 0 || symbol_len < 2 ||
+    if (!fmt_ok(in_fmt) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0 || symbol_len < 2 ||
         (symbol_len & 1))
         return OFS_EINVAL;
     if (B == 0 || T - symbol_len + 1 <= 0) return OFS_OK;
@@ -1022,7 +1024,8 @@ int32_t ofs_win_plan(int32_t kind, int32_t in_fmt, int32_t precision, int32_t n_
 int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                    const int64_t* starts, int32_t n_fft, int32_t cp_len, double fs_hz,
                    double* P_out, double* cfo_out, void* stream) {
-    if (!fmt_ok(in_fmt) || !x || !starts || !cfo_out || B < 0 || n_br < 1 || T < 0 || n_fft < 1 || cp_len < 0)
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || OFS_MISSING(starts, B) || OFS_MISSING(cfo_out, B) || B < 0 ||
+        n_br < 1 || T < 0 || n_fft < 1 || cp_len < 0)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     hipStream_t st = (hipStream_t)stream;

@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// a required pointer may be null only when the buffer it describes is empty (B = 0, T = 0)
+#define OFS_MISSING(p, n) ((p) == nullptr && (int64_t)(n) > 0)
+
 namespace ofs {
 
 // ---- cross-lane (wave64) helpers: DPP row shifts + row broadcasts (GFX9-family DPP) ----

@@ -362,7 +362,7 @@ extern "C" {
 
 int32_t ofs_trailing_average(int32_t precision, const void* x, int64_t B, int64_t n, int32_t win,
                              int32_t clip_negative, double* out, void* stream) {
-    if (!real_ok(precision) || !x || !out || B < 0 || n < 0) return OFS_EINVAL;
+    if (!real_ok(precision) || OFS_MISSING(x, B * n) || OFS_MISSING(out, B * n) || B < 0 || n < 0) return OFS_EINVAL;
     if (B == 0 || n == 0) return OFS_OK;
     const dim3 grid((unsigned)((B + PW / 64 - 1) / (PW / 64)));
     hipStream_t st = (hipStream_t)stream;
@@ -376,7 +376,8 @@ int32_t ofs_trailing_average(int32_t precision, const void* x, int64_t B, int64_
 int32_t ofs_plateau_end(int32_t precision, const void* M, int64_t B, int64_t n, int32_t cp_len,
                         int32_t lookahead, int32_t smooth_win, double* Ms, int64_t* plateau_end,
                         int32_t* status, void* stream) {
-    if (!real_ok(precision) || (!M && n > 0) || !Ms || !plateau_end || !status || B < 0 || n < 0 || cp_len < 0)
+    if (!real_ok(precision) || OFS_MISSING(M, B * n) || OFS_MISSING(Ms, B * n) || OFS_MISSING(plateau_end, B) ||
+        OFS_MISSING(status, B) || B < 0 || n < 0 || cp_len < 0)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     if (B > 0x7fffffff) return OFS_EINVAL;
@@ -390,7 +391,8 @@ int32_t ofs_plateau_end(int32_t precision, const void* M, int64_t B, int64_t n, 
 int32_t ofs_minn_peak(const double* Ms, int64_t B, int64_t n, double gate_threshold, int64_t bound_lo,
                       int64_t bound_hi, int64_t* peak, int64_t* gate_lo, int64_t* gate_hi, int32_t* status,
                       void* stream) {
-    if ((!Ms && n > 0) || !peak || !status || B < 0 || n < 0 || B > 0x7fffffff) return OFS_EINVAL;
+    if (OFS_MISSING(Ms, B * n) || OFS_MISSING(peak, B) || OFS_MISSING(status, B) || B < 0 || n < 0 || B > 0x7fffffff)
+        return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     hipLaunchKernelGGL(minn_peak_kernel, dim3((unsigned)B), dim3(PW), 0, (hipStream_t)stream, Ms, n,
                        gate_threshold, bound_lo, bound_hi, peak, gate_lo, gate_hi, status);
@@ -399,7 +401,7 @@ int32_t ofs_minn_peak(const double* Ms, int64_t B, int64_t n, double gate_thresh
 
 int32_t ofs_sc_gate(int32_t precision, const void* M_sc, int64_t B, int64_t n, double threshold,
                     uint8_t* mask, int64_t* span, void* stream) {
-    if (!real_ok(precision) || (!M_sc && n > 0) || B < 0 || n < 0 || B > 0x7fffffff || (!mask && !span))
+    if (!real_ok(precision) || OFS_MISSING(M_sc, B * n) || B < 0 || n < 0 || B > 0x7fffffff || (!mask && !span && B > 0))
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -412,8 +414,8 @@ int32_t ofs_sc_gate(int32_t precision, const void* M_sc, int64_t B, int64_t n, d
 
 int32_t ofs_segment_peak(const double* Ms, const uint8_t* mask, int64_t B, int64_t n, int64_t bound_lo,
                          int64_t bound_hi, int64_t* peak, int32_t* status, void* stream) {
-    if ((!Ms || !mask) && n > 0) return OFS_EINVAL;
-    if (!peak || !status || B < 0 || n < 0 || B > 0x7fffffff || bound_lo < 0 || bound_hi > n) return OFS_EINVAL;
+    if ((!Ms || !mask) && n > 0 && B > 0) return OFS_EINVAL;
+    if (OFS_MISSING(peak, B) || OFS_MISSING(status, B) || B < 0 || n < 0 || B > 0x7fffffff || bound_lo < 0 || bound_hi > n) return OFS_EINVAL;
     if (B == 0) return OFS_OK;
     hipLaunchKernelGGL(segment_peak_kernel, dim3((unsigned)B), dim3(PW), 0, (hipStream_t)stream, Ms, mask, n,
                        bound_lo, bound_hi, peak, status);

@@ -147,6 +147,12 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
         raise ValueError("Received stream is shorter than a single OFDM symbol.")
     prec = _lib.FP32 if batch.fmt == _lib.C64 else _lib.FP64
     dev = batch.data.device
+    if batch.B == 0:                                   # empty batch: nothing to transform
+        out = torch.empty((0, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
+        if return_peak:
+            return (out, torch.empty((0,), dtype=torch.int64, device=dev),
+                    torch.empty((0,), dtype=torch.float64, device=dev))
+        return out
     plan = _plan(prec, N, batch.B * batch.nb, batch.T)
     spec = torch.empty((batch.B * batch.nb, N), dtype=batch.data.dtype, device=dev)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None

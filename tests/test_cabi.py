@@ -90,6 +90,18 @@ def test_argument_validation_without_gpu(lib):
     # empty batches are valid no-ops
     assert lib.ofs_sc_metric(0, 1, 0, 1, 16, 8, 0, 0, None, None, None, None) == 0
     assert lib.ofs_minn_metric(0, 1, 1, 1, 4, 8, 0, None, None, None, None) == 0
+    # ... and their pointers may be NULL (no data behind them): B = 0 with every array null
+    assert lib.ofs_aa_detect(0, None, 0, 1, 1024, 512, 0, None, None, None, None, 1, 0.15, 128, 15.36e6, 4,
+                             None, None, None, None) == 0
+    assert lib.ofs_sc_metric(0, None, 0, 1, 4096, 2048, 1, 0, None, None, None, None) == 0
+    assert lib.ofs_sc_minn_metric(0, None, 0, 1, 4096, 2048, 0, None, None, None, None, None, None, None) == 0
+    assert lib.ofs_minn_rtl(2, None, 0, 1, 1024, 64, 3, 0, 3276, 15, None, None, None, None, None, None,
+                            None, None, 1, 2, 0, 4, None, None, None, None) == 0
+    assert lib.ofs_cp_cfo(0, None, 0, 1, 16, None, 8, 4, 1.0, None, None, None) == 0
+    assert lib.ofs_trailing_average(1, None, 0, 100, 8, 0, None, None) == 0
+    # a null pointer for a NON-empty buffer is still refused
+    assert lib.ofs_aa_detect(0, None, 1, 1, 1024, 512, 0, None, None, None, None, 0, 0.15, 128, 15.36e6, 0,
+                             None, None, None, None) == -1
 
 
 def test_product_path_refuses_cpu():
