@@ -108,7 +108,7 @@ __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1
     constexpr int PD = E <= 2 ? 4 : 2;                       // rows in flight ahead of use
     constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * (XA / 64) + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)xcd_block_w() * (XA / 64) + (threadIdx.x >> 6);
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int nrows = (int)((T + RL - 1) / RL);

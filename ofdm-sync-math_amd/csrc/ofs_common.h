@@ -120,6 +120,18 @@ __device__ __forceinline__ unsigned xcd_block() {
 #endif
 }
 
+// the same order for the other wave-per-stream kernels (tuning builds: -DOFS_XCD_WIDE=1)
+#ifndef OFS_XCD_WIDE
+#define OFS_XCD_WIDE 0
+#endif
+__device__ __forceinline__ unsigned xcd_block_w() {
+#if OFS_XCD_WIDE
+    return xcd_block();
+#else
+    return blockIdx.x;
+#endif
+}
+
 // atan2 in fp32 to ~1.5e-7 rad: odd degree-15 polynomial on [0, 1] (fitted to atan, fp32
 // coefficients) plus octant reduction; ~25 VALU instead of ocml's ~125.  Used where the inputs
 // are fp32 results anyway (the fast path's CFO from an fp32 P).

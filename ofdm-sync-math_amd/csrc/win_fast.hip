@@ -42,7 +42,7 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     constexpr int PER = HR > PD ? HR : PD;                   // unroll period (ring sizes divide it)
     constexpr int V4 = E / 2;                                // float4 loads per lane per row
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * (WF_WG / 64) + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)xcd_block_w() * (WF_WG / 64) + (threadIdx.x >> 6);
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
@@ -238,7 +238,7 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     __shared__ float hist[WF_WG / 64][ER + 2 * XR][E][64];   // [S_e rows | S_q re rows | S_q im rows]
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)blockIdx.x * (WF_WG / 64) + w;
+    const int64_t b = (int64_t)xcd_block_w() * (WF_WG / 64) + w;
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
