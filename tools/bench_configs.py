@@ -53,6 +53,24 @@ def batch_arena(dev, specs, contiguous):
     return _lib.arena(dev, specs, contiguous=False)
 
 
+def dbuf(dev, shape, dtype):
+    """A config buffer: its own physically contiguous block when OFS_BENCH_ALLOC=contig (the
+    headline's layout since r01i), else a plain torch allocation."""
+    if os.environ.get("OFS_BENCH_ALLOC", "plain") == "contig":
+        try:
+            return _lib.arena(dev, [(tuple(shape), dtype)], contiguous=True)[0]
+        except MemoryError:
+            pass
+    return torch.empty(shape, dtype=dtype, device=dev)
+
+
+def dput(dev, t):
+    """Move an input batch into a dbuf."""
+    b = dbuf(dev, t.shape, t.dtype)
+    b.copy_(t)
+    return b
+
+
 def chk(rc, what):
     if rc:
         raise RuntimeError(f"{what}: status {rc}")
@@ -68,11 +86,11 @@ def int12(x):
 def cfg2a(dev, st, steps, warmup):
     """cfg2 (aa side): sync_aa detector, L=128, int12 I/Q, B=4096 x T=1024, fp64 (bit-exact)."""
     B, T, L = 4096, 1024, 128
-    x = int12(synth.make_aa_batch(B, T, L, seed=7, device=dev))
-    P = torch.empty((B, T), dtype=torch.complex128, device=dev)
-    R = torch.empty((B, T), dtype=torch.float64, device=dev)
-    M = torch.empty_like(R)
-    V = torch.empty((B, T), dtype=torch.uint8, device=dev)
+    x = dput(dev, int12(synth.make_aa_batch(B, T, L, seed=7, device=dev)))
+    P = dbuf(dev, (B, T), torch.complex128)
+    R = dbuf(dev, (B, T), torch.float64)
+    M = dbuf(dev, (B, T), torch.float64)
+    V = dbuf(dev, (B, T), torch.uint8)
     E = 4
     n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
     ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
@@ -123,10 +141,9 @@ def cfg2b(dev, st, steps, warmup):
 def cfg4(dev, st, steps, warmup):
     """cfg4 per-GPU shard: combined S&C (both-halves R) + Minn, N=2048, 32768 x 4096 c64, fp32."""
     B, T, N = 32768, 4096, 2048
-    x = synth.make_aa_batch(B, T, N // 2, seed=4, device=dev)
+    x = dput(dev, synth.make_aa_batch(B, T, N // 2, seed=4, device=dev))
     n_out = T - N + 1
-    outs = [torch.empty((B, n_out), dtype=dt, device=dev)
-            for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    outs = [dbuf(dev, (B, n_out), dt) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
     L_ = _lib.lib()
 
     fused = os.environ.get("OFS_CFG4_SEPARATE", "0") != "1"
@@ -209,10 +226,10 @@ def cfg3_2ant(dev, st, steps, warmup):
     """cfg3 with two receive antennas per stream (sync_aa's run_single_test uses 2 RX): 65536 x
     2 x 1024 c64, L=512, fp32 fast path, events fused."""
     B, T, L, E = 65536, 1024, 512, 4
-    x = synth.synth_batch(synth.faded_base(L, "cir1", (0, 1)), B, T, seed=32, device=dev)
-    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
-    R = torch.empty((B, T), dtype=torch.float32, device=dev)
-    M = torch.empty_like(R)
+    x = dput(dev, synth.synth_batch(synth.faded_base(L, "cir1", (0, 1)), B, T, seed=32, device=dev))
+    P = dbuf(dev, (B, T), torch.complex64)
+    R = dbuf(dev, (B, T), torch.float32)
+    M = dbuf(dev, (B, T), torch.float32)
     n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
     ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
     ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
@@ -231,9 +248,9 @@ def cfg4_2br(dev, st, steps, warmup):
     """cfg4 with two receive branches per stream (combined_sc_min.run_simulation feeds cir1[:2]):
     16384 x 2 x 4096 c64, N = 2048, fused S&C + Minn."""
     B, T, N = 16384, 4096, 2048
-    x = synth.synth_batch(synth.faded_base(N // 2, "cir1", (0, 1)), B, T, seed=42, device=dev)
+    x = dput(dev, synth.synth_batch(synth.faded_base(N // 2, "cir1", (0, 1)), B, T, seed=42, device=dev))
     n_out = T - N + 1
-    outs = [torch.empty((B, n_out), dtype=dt, device=dev) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    outs = [dbuf(dev, (B, n_out), dt) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
     L_ = _lib.lib()
     ms = timed(lambda: chk(L_.ofs_sc_minn_metric(_lib.C64, x.data_ptr(), B, 2, T, N, _lib.FP32,
                                                  *[t.data_ptr() for t in outs], st.cuda_stream), "sc_minn 2br"),
@@ -247,10 +264,10 @@ def cfg3_fp64(dev, st, steps, warmup):
     """cfg3 shape in the reference's float64 (complex128 in, f64/c128 out: the numpy drop-in's
     precision), 65536 x 1024, L = 512, events fused."""
     B, T, L, E = 65536, 1024, 512, 4
-    x = synth.make_aa_batch(B, T, L, seed=33, device=dev, dtype=torch.complex128)
-    P = torch.empty((B, T), dtype=torch.complex128, device=dev)
-    R = torch.empty((B, T), dtype=torch.float64, device=dev)
-    M = torch.empty_like(R)
+    x = dput(dev, synth.make_aa_batch(B, T, L, seed=33, device=dev, dtype=torch.complex128))
+    P = dbuf(dev, (B, T), torch.complex128)
+    R = dbuf(dev, (B, T), torch.float64)
+    M = dbuf(dev, (B, T), torch.float64)
     n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
     ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
     ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
