@@ -53,6 +53,9 @@ extern "C" {
 #define OFS_ZC_SUM        4   /* sum_br raw corr (detect_zc_preamble, normalize=False)       */
 
 int32_t ofs_version(void);
+/* sha256 (16 hex digits) of the csrc sources (.hip, .h) and include/ofdmsync.h this library was
+ * built from ("unknown" for a build without it). */
+const char* ofs_source_hash(void);
 const char* ofs_status_string(int32_t status);
 
 /*

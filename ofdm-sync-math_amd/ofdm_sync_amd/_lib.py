@@ -22,11 +22,36 @@ FP32, FP64 = 0, 1
 
 _lib = None
 
+_CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+_HDR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "ofdmsync.h")
+
+
+def source_files() -> list[str]:
+    """The sources libofdmsync.so is compiled from (csrc .hip/.h + the ABI header)."""
+    if not os.path.isdir(_CSRC):
+        return []
+    fs = sorted(os.path.join(_CSRC, f) for f in os.listdir(_CSRC) if f.endswith((".hip", ".h")))
+    return fs + ([_HDR] if os.path.exists(_HDR) else [])
+
+
+def source_hash() -> str:
+    """sha256 (16 hex digits) over the sources' names and bytes: baked into the library at
+    build time (OFS_SOURCE_HASH) and checked at load, so a library built from other sources
+    than the ones next to it is refused instead of silently run."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 
 def _declare(lib):
     P = c_void_p
     sig = {
         "ofs_version": (c_int32, []),
+        "ofs_source_hash": (ctypes.c_char_p, []),
         "ofs_status_string": (ctypes.c_char_p, [c_int32]),
         "ofs_aa_detect": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P, P,
                                     P, c_int32, c_double, c_int32, c_double, c_int32, P, P, P, P]),
@@ -92,6 +117,11 @@ def lib():
                 "from the repository root (hipcc --offload-arch=gfx950)")
         l = ctypes.CDLL(LIB_PATH)
         _declare(l)
+        if not os.environ.get("OFS_LIB") and source_files():
+            built, want = l.ofs_source_hash().decode(), source_hash()
+            if built != want:
+                raise ImportError(f"{LIB_PATH} was built from other sources (hash {built}, sources {want}); "
+                                  "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
         _lib = l
     return _lib
 

@@ -77,15 +77,37 @@ class AABatchResult:
     ev_real: torch.Tensor | None
 
 
+PLACEMENTS = ("plain", "contiguous")
+
+
+def allocate(dev, specs, placement: str = "plain"):
+    """Device buffers for a batch: ``specs`` = list of (shape, dtype) or None.
+
+    placement "plain": one allocation from torch's caching allocator, carved into 2 MiB-aligned
+    buffers; "contiguous": every buffer its own physically contiguous block
+    (hipExtMallocWithFlags(hipDeviceMallocContiguous)), freed with the tensor.  The headline
+    shape (cfg3, 1.6 GB per launch) runs 0.27-0.30 ms with "contiguous" against 0.30-0.33 ms
+    "plain" depending on the box; other shapes measured the opposite, hence a
+    per-call choice, default "plain".  Raises MemoryError if the driver cannot back a
+    contiguous block.
+    """
+    if placement == "plain":
+        return _lib.arena(dev, specs, contiguous=False)
+    if placement == "contiguous":
+        return [None if sp is None else _lib.arena(dev, [sp], contiguous=True)[0] for sp in specs]
+    raise ValueError(f"placement must be one of {PLACEMENTS}, got {placement!r}")
+
+
 def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_rate: float,
-         prec: int, want=("P", "R", "M", "valid"), detect: bool = True, max_events: int = 16):
+         prec: int, want=("P", "R", "M", "valid"), detect: bool = True, max_events: int = 16,
+         placement: str = "plain"):
     dev = batch.data.device
     B, T = batch.B, batch.T
     ct = torch.complex128 if prec == _lib.FP64 else torch.complex64
     rt = torch.float64 if prec == _lib.FP64 else torch.float32
-    P, R, M, V = _lib.arena(dev, [((B, T), ct) if "P" in want else None, ((B, T), rt) if "R" in want else None,
-                                  ((B, T), rt) if "M" in want else None,
-                                  ((B, T), torch.bool) if "valid" in want else None])
+    P, R, M, V = allocate(dev, [((B, T), ct) if "P" in want else None, ((B, T), rt) if "R" in want else None,
+                                ((B, T), rt) if "M" in want else None,
+                                ((B, T), torch.bool) if "valid" in want else None], placement)
     n_ev = ev_i = ev_r = None
     if detect:
         n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
@@ -100,15 +122,78 @@ def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_ra
     return AABatchResult(P, R, M, V, n_ev, ev_i, ev_r)
 
 
+class AABatchDetector:
+    """Preallocated, launch-only form of ``aa_detect_streaming_batched`` (serving / benchmark use).
+
+    Buffers for a fixed shape [B, n_ant, T] are allocated once (``placement``: see
+    ``allocate``); ``run()`` enqueues ONE ``ofs_aa_detect`` launch on the current stream and
+    returns without a host synchronisation, so back-to-back calls pipeline on the GPU.  Event
+    slots are ``max_events`` per stream; ``overflowed()`` (synchronising) reports whether any
+    stream produced more (its count stays exact in ``n_events``; the batched function re-runs
+    in that case, this class leaves it to the caller).
+    """
+
+    def __init__(self, B: int, T: int, n_ant: int = 1, L: int = PREAMBLE_HALF_LEN,
+                 threshold: float = DETECT_THRESHOLD, hysteresis: int = DETECT_HYSTERESIS,
+                 sample_rate: float = SAMPLE_RATE_HZ, *, precision="fp32", in_dtype=None,
+                 outputs=("P", "R", "M"), detect: bool = True, max_events: int = 4,
+                 placement: str = "plain", device=None):
+        dev = torch.device(device) if device is not None else _lib.require_gpu()
+        _lib.lib()
+        prec = _lib.resolve_precision(_lib.Batch(None, _lib.C64, B, n_ant, T, False, False), precision)
+        if in_dtype is None:
+            in_dtype = torch.complex64 if prec == _lib.FP32 else torch.complex128
+        self.fmt = {torch.complex64: _lib.C64, torch.complex128: _lib.C128, torch.int16: _lib.CI16}[in_dtype]
+        ct = torch.complex128 if prec == _lib.FP64 else torch.complex64
+        rt = torch.float64 if prec == _lib.FP64 else torch.float32
+        xshape = (B, n_ant, T, 2) if in_dtype == torch.int16 else (B, n_ant, T)
+        want = tuple(outputs)
+        if detect and B > 0 and T > 0 and _lib.lib().ofs_aa_plan(self.fmt, prec, n_ant, T, int(L)) == 2:
+            want = tuple(set(want) | {"P", "M"})         # tiled general engine: events from P/M in HBM
+        self.x, P, R, M, V = allocate(dev, [(xshape, in_dtype), ((B, T), ct) if "P" in want else None,
+                                            ((B, T), rt) if "R" in want else None,
+                                            ((B, T), rt) if "M" in want else None,
+                                            ((B, T), torch.bool) if "valid" in want else None], placement)
+        E = max(int(max_events), 1)
+        n_ev = torch.zeros((B,), dtype=torch.int32, device=dev) if detect else None
+        ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev) if detect else None
+        ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev) if detect else None
+        self.result = AABatchResult(P, R, M, V, n_ev, ev_i, ev_r)
+        self.B, self.T, self.n_ant, self.L, self.prec, self.max_events = B, T, n_ant, int(L), prec, E
+        self.placement, self.device = placement, dev
+        self._fn = _lib.lib().ofs_aa_detect
+        self._tail = (prec, _lib.ptr(P), _lib.ptr(R), _lib.ptr(M), _lib.ptr(V), int(detect), float(threshold),
+                      int(hysteresis), float(sample_rate), E, _lib.ptr(n_ev), _lib.ptr(ev_i), _lib.ptr(ev_r))
+
+    def plan(self) -> int:
+        """ofs_aa_plan of this shape (which kernel ``run`` launches)."""
+        return int(_lib.lib().ofs_aa_plan(self.fmt, self.prec, self.n_ant, self.T, self.L))
+
+    def run(self, x: torch.Tensor | None = None, stream: int | None = None) -> AABatchResult:
+        """Launch on the batch in ``x`` (default: the detector's own input buffer ``self.x``)."""
+        x = self.x if x is None else x
+        if x.device != self.device or not x.is_contiguous() or x.numel() != self.x.numel() or x.dtype != self.x.dtype:
+            raise ValueError("x must be a contiguous device tensor shaped and typed like AABatchDetector.x")
+        rc = self._fn(self.fmt, x.data_ptr(), self.B, self.n_ant, self.T, self.L, *self._tail,
+                      _lib.stream_ptr() if stream is None else stream)
+        _lib.check(rc, "ofs_aa_detect")
+        return self.result
+
+    def overflowed(self) -> bool:
+        n = self.result.n_events
+        return bool(n is not None and n.numel() and int(n.max().item()) > self.max_events)
+
+
 def aa_detect_streaming_batched(x, L: int = PREAMBLE_HALF_LEN, threshold: float = DETECT_THRESHOLD,
                                 hysteresis: int = DETECT_HYSTERESIS,
                                 sample_rate: float = SAMPLE_RATE_HZ, *, precision=None,
                                 outputs=("P", "R", "M", "valid"), detect: bool = True,
-                                max_events: int = 16) -> AABatchResult:
+                                max_events: int = 16, placement: str = "plain") -> AABatchResult:
     """Batched [A][A] detector over independent streams x[B, n_ant, T] (or [B, T]).
 
     Same per-stream semantics as ``aa_detect_streaming``; results stay on the GPU.
     ``precision``: None (fp64 for complex128/int16 input, fp32 for complex64), 'fp32', 'fp64'.
+    ``placement``: output backing, "plain" or "contiguous" (see ``allocate``).
     """
     batch = _lib.as_batch(x, batched=True)
     prec = _lib.resolve_precision(batch, precision)
@@ -117,11 +202,11 @@ def aa_detect_streaming_batched(x, L: int = PREAMBLE_HALF_LEN, threshold: float 
     # over P/M in HBM; every other plan keeps them on chip, so detect-only skips those stores
     if detect and batch.T > 0 and _lib.lib().ofs_aa_plan(batch.fmt, prec, batch.nb, batch.T, int(L)) == 2:
         want = tuple(sorted(set(want) | {"P", "M"}, key=["P", "R", "M", "valid"].index))
-    res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, max_events)
+    res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, max_events, placement)
     if detect and batch.B > 0 and batch.T > 0:
         worst = int(res.n_events.max().item())
         if worst > max_events:
-            res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, worst)
+            res = _run(batch, L, threshold, hysteresis, sample_rate, prec, want, detect, worst, placement)
     for name in ("P", "R", "M", "valid"):
         if name not in outputs:
             setattr(res, name, None)

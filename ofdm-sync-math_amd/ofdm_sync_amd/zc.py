@@ -21,8 +21,9 @@ generate_zadoff_chu = _v2.generate_zadoff_chu
 
 
 def build_pss_symbol(include_cp: bool = True) -> np.ndarray:
-    _v2.N_FFT, _v2.CYCLIC_PREFIX = N_FFT, CYCLIC_PREFIX
-    return _v2.build_pss_symbol(include_cp=include_cp)
+    """zc.py:39-47: this module's N_FFT / CYCLIC_PREFIX (read at call time), passed explicitly
+    so zc_v2's own module globals are never touched."""
+    return _v2.build_pss_symbol(include_cp=include_cp, n_fft=N_FFT, cyclic_prefix=CYCLIC_PREFIX)
 
 
 def combined_matched_filter(rx_samples, pss_reference=None, *, want_mag: bool = False):

@@ -42,17 +42,23 @@ def generate_zadoff_chu(root: int, length: int) -> np.ndarray:
     return np.exp(-1j * np.pi * root * n * (n + 1) / length)
 
 
-def build_pss_symbol(include_cp: bool = False) -> np.ndarray:
-    """ZC on the centered bins, unit-power time symbol (zc_v2.py:170-185, core.py:21-47)."""
+def build_pss_symbol(include_cp: bool = False, *, n_fft: int | None = None,
+                     cyclic_prefix: int | None = None) -> np.ndarray:
+    """ZC on the centered bins, unit-power time symbol (zc_v2.py:170-185, core.py:21-47).
+
+    ``n_fft`` / ``cyclic_prefix`` default to this module's N_FFT / CYCLIC_PREFIX read at call
+    time (the reference's module globals); passing them never mutates the globals."""
+    N = N_FFT if n_fft is None else int(n_fft)
+    cp = CYCLIC_PREFIX if cyclic_prefix is None else int(cyclic_prefix)
     idx = centered_subcarrier_indices(PSS_LENGTH)
-    spec = np.zeros(N_FFT, dtype=complex)
-    spec[(N_FFT // 2 + idx) % N_FFT] = generate_zadoff_chu(PSS_ROOT, PSS_LENGTH)
+    spec = np.zeros(N, dtype=complex)
+    spec[(N // 2 + idx) % N] = generate_zadoff_chu(PSS_ROOT, PSS_LENGTH)
     sym = np.fft.ifft(np.fft.ifftshift(spec))
     p = np.mean(np.abs(sym) ** 2)
     if p != 0:
         sym = sym / np.sqrt(p)
-    if include_cp and CYCLIC_PREFIX > 0:
-        sym = np.concatenate((sym[-CYCLIC_PREFIX:], sym))
+    if include_cp and cp > 0:
+        sym = np.concatenate((sym[-cp:], sym))
     return sym
 
 

@@ -124,6 +124,58 @@ def aa_detect(rx, L=512, threshold=0.15, hysteresis=128, sample_rate=15.36e6):
     return P, R, M, valid, ints, reals
 
 
+def aa_metric_loop(rx, L):
+    """Literal per-sample form of sync_aa.py:458-493 (DelayLine :368-386, RunningSum :321-342,
+    RunningSumReal :345-365 as ring buffers, one Python iteration per sample and antenna).
+
+    Same complexity as the reference (the "literal-loop" CPU baseline of bench.py); values
+    equal the reference's recursion bit for bit (same operation order, Python complex/float).
+    """
+    x = _as2d(rx)
+    na, T = x.shape
+    rows = [list(map(complex, x[a])) for a in range(na)]
+    dl = [[0j] * L for _ in range(na)]
+    pb = [[0j] * L for _ in range(na)]
+    rb = [[0.0] * L for _ in range(na)]
+    ps = [0j] * na
+    rs = [0.0] * na
+    ptr, filled = 0, 0
+    P = np.zeros(T, np.complex128)
+    R = np.zeros(T)
+    M = np.zeros(T)
+    valid = np.zeros(T, bool)
+    floor_ = 1e-6 * L
+    for n in range(T):
+        P_sum, R_sum = 0j, 0.0
+        ok = filled >= L                            # delay / window filled before this push
+        for a in range(na):
+            xn = rows[a][n]
+            xd = dl[a][ptr]
+            dl[a][ptr] = xn
+            prod = xn * xd.conjugate() if ok else 0j
+            ps[a] = ps[a] + prod - pb[a][ptr]
+            pb[a][ptr] = prod
+            pw = abs(xn) ** 2
+            rs[a] = rs[a] + pw - rb[a][ptr]
+            rb[a][ptr] = pw
+            P_sum += ps[a]
+            R_sum += rs[a]
+        ptr = ptr + 1 if ptr + 1 < L else 0
+        if filled < L:
+            filled += 1
+        P[n], R[n], valid[n] = P_sum, R_sum, ok
+        if ok and R_sum > floor_:
+            M[n] = min(abs(P_sum) ** 2 / R_sum ** 2, 1.0)
+    return P, R, M, valid
+
+
+def aa_detect_loop(rx, L=512, threshold=0.15, hysteresis=128, sample_rate=15.36e6):
+    """aa_detect in the reference's literal streaming form (aa_metric_loop + aa_events)."""
+    P, R, M, valid = aa_metric_loop(rx, L)
+    ints, reals = aa_events(P, M, valid, L, threshold, hysteresis, sample_rate)
+    return P, R, M, valid, ints, reals
+
+
 # ---------------------------------------------------------------------------------------
 # sc.sc_streaming_metric (sc.py:42-78) and combined_sc_min.schmidl_cox_streaming_metric
 # (combined_sc_min.py:116-164)

@@ -249,3 +249,24 @@ def test_closed_form_events_equal_loop_fsm(seed):
     cf_i, cf_r = events_closed_form(P, M, valid, L, thr, hyst, 15.36e6)
     assert np.array_equal(ref_i, cf_i)
     assert np.allclose(ref_r, cf_r)
+
+
+@pytest.mark.parametrize("case", ["aa_clean_L512", "aa_cfo_L512", "aa_grid_len1024_cir1_snr0_fs0.5",
+                                  "aa_grid_len256_cir1_snr0_fs1.0", "aa_edge_T15_L8_a2", "aa_edge_T33_L2_a2",
+                                  "aa_edge_T5_L8_a1", "aa_int12_L128"])
+def test_literal_loop_form_matches_reference_golden(case):
+    """The literal per-sample restatement (bench.py's literal-loop CPU baseline) reproduces the
+    reference's own outputs: same recursion, so ~ulp agreement (bit-exact on int12 inputs)."""
+    d = _load(os.path.join(GOLDEN, case + ".npz"))
+    L = int(d["L"])
+    P, R, M, valid, ei, er = O.aa_detect_loop(d["x"], L, float(d["threshold"]), int(d["hysteresis"]),
+                                              float(d["sample_rate"]))
+    scale = max(1.0, float(np.max(np.abs(d["R"]))))
+    assert np.max(np.abs(P - d["P"]), initial=0) <= 1e-12 * scale
+    assert np.max(np.abs(R - d["R"]), initial=0) <= 1e-12 * scale
+    assert np.max(np.abs(M - d["M"]), initial=0) <= 1e-12
+    assert np.array_equal(valid, d["valid"])
+    assert np.array_equal(ei, d["ev_int"].reshape(-1, 4))
+    assert np.allclose(er, d["ev_real"].reshape(-1, 4), rtol=1e-12, atol=1e-9)
+    if case == "aa_int12_L128":
+        assert np.array_equal(P, d["P"]) and np.array_equal(R, d["R"])
