@@ -78,10 +78,12 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
  * Which kernel ofs_aa_detect dispatches a shape to (pure query, no launch):
  *   1000 + 10*E + MR : register-resident wave-per-stream fast path (E samples per lane,
  *                      L = 64*E*MR), complex64 / OFS_FP32 / 1-2 antennas / even T <= 1024;
+ *   1100 + 10*E + MR : streaming wave-per-stream fast path, same arithmetic, any other T
+ *                      (rows streamed from HBM, lag / window rings in registers), MR <= 8;
  *   2000 + 10*E + MR : integer-exact wave-per-stream path, OFS_CI16 / OFS_FP64, 1-2 antennas,
  *                      T * n_ant <= 2^21 (all window sums exact integers), L = 64*E*MR, MR <= 8;
  *   3000 + 10*E + MR : the same wave-per-stream kernel on OFS_C128 / OFS_FP64 input (fp64 prefix
- *                      differences over the stream, T <= 3584 = the general engine's fp64 tile);
+ *                      differences over the stream, any T: the reference's running-sum error regime);
  *   1                : general LDS engine, events fused (stream fits one tile);
  *   2                : general LDS engine, tiled, events in a second pass over P/M;
  *   <0               : invalid arguments or window too long (as ofs_aa_detect would return).

@@ -245,6 +245,218 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     if (a.detect) gate.finish(lane, T, a.n_ev + b);
 }
 
+// ------------------------------------------------------------------------------------------
+// Streaming variant for ANY stream length (T > 1024 or odd T: the reference's own detector
+// input, sync_aa.run_single_test, is ~4.2-5.3k samples x 2 antennas, sync_aa.py:699-738).
+// Same row layout, window split and gate machine as aa_fast_kernel; instead of holding the
+// whole stream in registers, rows stream from HBM PD rows ahead of use and only what the
+// window needs is retained: the raw samples of rows k-MR..k-1 (lag L = MR rows), the fp32
+// in-window suffixes of those rows and the fp64 row bases C[k-MR+1..k] (register rings
+// indexed by k mod MR, resolved at compile time by unrolling the row loop by the ring period).
+// Odd T: the stream base is only 8-byte aligned, so pair loads/stores use 8-byte-aligned
+// vector types (gfx950 global memory ops need dword alignment only) and the last, partial row
+// falls back to per-sample accesses.
+// ------------------------------------------------------------------------------------------
+typedef float f4u __attribute__((ext_vector_type(4), aligned(8)));
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+
+#ifndef OFS_STREAM_WG
+#define OFS_STREAM_WG 64
+#endif
+constexpr int STREAM_WG = OFS_STREAM_WG;
+// tuning builds: rows in flight (OFS_STREAM_PD), occupancy bound (OFS_STREAM_WAVES waves/SIMD)
+#ifndef OFS_STREAM_PD
+#define OFS_STREAM_PD 0
+#endif
+#ifndef OFS_STREAM_WAVES
+#define OFS_STREAM_WAVES 0
+#endif
+#if OFS_STREAM_WAVES > 0
+#define OFS_STREAM_BOUNDS __launch_bounds__(STREAM_WG, OFS_STREAM_WAVES)
+#else
+#define OFS_STREAM_BOUNDS __launch_bounds__(STREAM_WG)
+#endif
+
+template <int E, int MR, int NA, bool DO>
+__global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
+    constexpr int RL = 64 * E;
+    constexpr int L = MR * RL;
+    constexpr int V4 = E / 2;                                // sample pairs per lane per row
+    constexpr int PD = OFS_STREAM_PD > 0 ? OFS_STREAM_PD : (E == 2 ? 4 : 2);   // rows in flight ahead of use
+    constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)xcd_block() * (STREAM_WG / 64) + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int Ti = (int)T;
+    const int nrows = (int)((T + RL - 1) / RL);
+    const int full_rows = (int)(T / RL);                     // rows entirely inside the stream
+    const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NA * T;
+
+    float lr[NA][MR][E], li[NA][MR][E];                      // x of rows k-MR..k-1 (lag L)
+    float sR[MR][E], sI[MR][E], sE[MR][E];                   // retained in-window suffixes
+    double cbR[MR], cbI[MR], cbE[MR];                        // row bases C[j], j in (k-MR, k]
+    double CR = 0.0, CI = 0.0, CE = 0.0;                     // C[k]: prefix at the start of row k
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        cbR[m] = 0.0; cbI[m] = 0.0; cbE[m] = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f;
+#pragma unroll
+            for (int t = 0; t < NA; ++t) { lr[t][m][e] = 0.f; li[t][m][e] = 0.f; }
+        }
+    }
+
+    // a row's samples of one antenna: pairs as 8-byte-aligned float4 for whole rows, else
+    // per-sample with zero fill past T
+    float2 nx[PD][NA][E];
+    auto load_row = [&](int k, float2 (&dst)[NA][E]) {
+        const int64_t n0 = (int64_t)RL * k + E * lane;
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            const float2* xs = xb + (int64_t)t * T;
+            if (k < full_rows) {
+#pragma unroll
+                for (int j = 0; j < V4; ++j) {
+                    const f4u v = *reinterpret_cast<const f4u*>(xs + n0 + 2 * j);
+                    dst[t][2 * j] = make_float2(v.x, v.y);
+                    dst[t][2 * j + 1] = make_float2(v.z, v.w);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) dst[t][e] = (n0 + e < T) ? xs[n0 + e] : make_float2(0.f, 0.f);
+            }
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+        if (p < nrows) load_row(p, nx[p]);
+
+    AaRowGate<E, float, false, DO> gate;
+    if (a.detect)
+        gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
+                  a.ev_r + b * (int64_t)a.max_ev * 4);
+    float2* Pout = DO ? nullptr : reinterpret_cast<float2*>(a.P);
+    float* Rout = DO ? nullptr : reinterpret_cast<float*>(a.R);
+    float* Mout = DO ? nullptr : reinterpret_cast<float*>(a.M);
+    uint8_t* Vout = DO ? nullptr : a.valid;
+    const float floor_ = 1e-6f * (float)L;
+
+    for (int k0 = 0; k0 < nrows; k0 += PER) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = k0 + u;
+            if (k < nrows) {
+                const int nb = RL * k + E * lane;
+                const int sl = u % MR;                       // ring slot of row k-MR (and k)
+                float2 cur[NA][E];
+#pragma unroll
+                for (int t = 0; t < NA; ++t)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) cur[t][e] = nx[u % PD][t][e];
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
+                // ---- lagged products x[n]·conj(x[n-L]) and energies, summed over the antennas ----
+                float aR[E], aI[E], aE[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+#pragma unroll
+                for (int t = 0; t < NA; ++t)
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const float cr = cur[t][e].x, ci = cur[t][e].y;
+                        aE[e] += fmaf(cr, cr, ci * ci);
+                        if (k >= MR) {
+                            aR[e] += fmaf(cr, lr[t][sl][e], ci * li[t][sl][e]);
+                            aI[e] += fmaf(ci, lr[t][sl][e], -(cr * li[t][sl][e]));
+                        }
+                        lr[t][sl][e] = cr; li[t][sl][e] = ci;
+                    }
+                // ---- in-lane partials (forward f, backward g), fp64 wave scan ----
+                float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
+                fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+#pragma unroll
+                for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
+                gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+#pragma unroll
+                for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+                const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
+                const double tR = readlane(iR, 63), tI = readlane(iI, 63), tE = readlane(iE, 63);
+                const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);
+                const float uR = (float)(tR - iR), uI = (float)(tI - iI), uE = (float)(tE - iE);
+                const int so = (u + 1) % MR;                 // slot of C[k-MR+1]
+                const float wR = (float)(k >= MR ? CR - cbR[so] : CR);
+                const float wI = (float)(k >= MR ? CI - cbI[so] : CI);
+                const float wE = (float)(k >= MR ? CE - cbE[so] : CE);
+                // ---- window sums P = suffix(row k-MR) + rows between + prefix(row k) ----
+                float pr[E], pi[E], rf[E], mf[E], pmf[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    float PR = wR + (xR + fR[e]), PI = wI + (xI + fI[e]), RR = wE + (xE + fE[e]);
+                    if (k >= MR) { PR += sR[sl][e]; PI += sI[sl][e]; RR += sE[sl][e]; }
+                    sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
+                    const float pm = fmaf(PR, PR, PI * PI);
+                    float m = 0.f;
+                    if (k >= MR && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
+                    pr[e] = PR; pi[e] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
+                }
+                cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
+                CR += tR; CI += tI; CE += tE;
+                // ---- stores ----
+                if (!DO) {
+                    const int64_t o = b * T + nb;
+                    if (k < full_rows) {
+#pragma unroll
+                        for (int j = 0; j < V4; ++j) {
+                            if (Pout) *reinterpret_cast<f4u*>(Pout + o + 2 * j) = f4u{pr[2 * j], pi[2 * j], pr[2 * j + 1], pi[2 * j + 1]};
+                            if (Rout) *reinterpret_cast<f2u*>(Rout + o + 2 * j) = f2u{rf[2 * j], rf[2 * j + 1]};
+                            if (Mout) *reinterpret_cast<f2u*>(Mout + o + 2 * j) = f2u{mf[2 * j], mf[2 * j + 1]};
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e)
+                            if (nb + e < Ti) {
+                                if (Pout) Pout[o + e] = make_float2(pr[e], pi[e]);
+                                if (Rout) Rout[o + e] = rf[e];
+                                if (Mout) Mout[o + e] = mf[e];
+                            }
+                    }
+                    if (Vout) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e)
+                            if (nb + e < Ti) Vout[o + e] = (uint8_t)(k >= MR);
+                    }
+                }
+                // ---- events: closed-form gate machine, streamed per row (aa_gate.h) ----
+                if (a.detect && k >= MR) gate.row(lane, k, nb, Ti, mf, pmf, pr, pi);
+            }
+        }
+    }
+    if (a.detect) gate.finish(lane, Ti, a.n_ev + b);
+}
+
+template <int E, int MR, int NA>
+int launch_stream(const AaFastArgs& a, hipStream_t st) {
+    const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
+    const int64_t grid = (a.B + STREAM_WG / 64 - 1) / (STREAM_WG / 64);
+    if (det_only)
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(STREAM_WG), 0, st, a);
+    else
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(STREAM_WG), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
+
+template <int E, int NA>
+int launch_stream_mr(int mr, const AaFastArgs& a, hipStream_t st) {
+    switch (mr) {
+        case 1: return launch_stream<E, 1, NA>(a, st);
+        case 2: return launch_stream<E, 2, NA>(a, st);
+        case 4: return launch_stream<E, 4, NA>(a, st);
+        case 8: return launch_stream<E, 8, NA>(a, st);
+    }
+    return 0;
+}
+
 template <int E, int MR, int NA>
 int launch(const AaFastArgs& a, hipStream_t st) {
     const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
@@ -291,18 +503,32 @@ int pick_e(int L) {
 
 }  // namespace
 
+// 10*E + MR of the register-staged kernel (even T <= 1024), 100 + 10*E + MR of the streaming
+// kernel (any other T), 0 if the general engine handles the shape
 int ofs_aa_fast_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
     if (fmt != OFS_C64 || precision != OFS_FP32) return 0;
     if (n_ant != 1 && n_ant != 2) return 0;
-    if (T < 2 || T > TMAX || (T & 1)) return 0;
-    if (L < 128 || L > TMAX) return 0;
-    const int E = pick_e(L);
-    if (!E) return 0;
-    return 10 * E + L / (64 * E);
+    if (T < 1 || L < 128) return 0;
+    if (T <= TMAX && !(T & 1) && L <= TMAX) {
+        const int E = pick_e(L);
+        if (E) return 10 * E + L / (64 * E);
+    }
+    if (T > 0x7fffffff - 1024) return 0;                     // row indices in int
+    for (int e : {2, 4}) {                                   // streaming: window of 1, 2, 4 or 8 rows
+        if (L % (64 * e)) continue;
+        const int mr = L / (64 * e);
+        if (mr == 1 || mr == 2 || mr == 4 || mr == 8) return 100 + 10 * e + mr;
+    }
+    return 0;
 }
 
 int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipStream_t st) {
     const int plan = ofs_aa_fast_plan(fmt, precision, n_ant, a.T, a.L);
     if (!plan) return 0;
+    if (plan >= 100) {
+        const int E = (plan - 100) / 10, mr = plan % 10;
+        if (E == 2) return n_ant == 1 ? launch_stream_mr<2, 1>(mr, a, st) : launch_stream_mr<2, 2>(mr, a, st);
+        return n_ant == 1 ? launch_stream_mr<4, 1>(mr, a, st) : launch_stream_mr<4, 2>(mr, a, st);
+    }
     return n_ant == 1 ? launch_e<1>(plan / 10, plan % 10, a, st) : launch_e<2>(plan / 10, plan % 10, a, st);
 }

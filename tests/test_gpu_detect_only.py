@@ -29,7 +29,9 @@ def _batch(kind, B, T, L):
 
 @pytest.mark.parametrize("kind,T,L,plan_lo,plan_hi", [("c64", 1024, 512, 1000, 2000), ("ci16", 1024, 128, 2000, 3000),
                                                        ("c128", 1024, 512, 3000, 4000),
-                                                       ("c128", 3000, 256, 3000, 4000), ("c128", 9000, 512, 2, 2)])
+                                                       ("c128", 3000, 256, 3000, 4000), ("c128", 9000, 512, 3000, 4000),
+                                                       ("c64", 4096, 512, 1100, 1200), ("c64", 5315, 256, 1100, 1200),
+                                                       ("c64", 9000, 100, 2, 2)])
 def test_detect_only_events_equal_full(kind, T, L, plan_lo, plan_hi):
     B = 512
     x = _batch(kind, B, T, L)

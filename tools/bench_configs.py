@@ -361,7 +361,47 @@ def cfg3_pcie(dev, st, steps, warmup):
                 alg_bytes=B * T * 24, bytes_per_sample="8 H2D + 16 D2H (PCIe) per sample")
 
 
-CONFIGS = {"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
+def _aa_cfg(dev, st, steps, warmup, name, B, na, T, L, dtype, prec, workload, seed):
+    """sync_aa detector on a [B, na, T] batch through the product's AABatchDetector (plain
+    placement), P/R/M + events; algorithmic bytes = input + P/R/M per time index."""
+    from ofdm_sync_amd import sync_aa
+    det = sync_aa.AABatchDetector(B, T, na, L, precision=prec, in_dtype=dtype, outputs=("P", "R", "M"),
+                                  max_events=4, device=dev)
+    base = synth.faded_base(L, "cir1", tuple(range(na)) if na > 1 else (1,))
+    det.x.copy_(synth.synth_batch(base, B, T, seed=seed, device=dev, dtype=dtype))
+    ms = timed(lambda: det.run(), steps, warmup, st)
+    esz = 8 if dtype == torch.complex64 else 16
+    osz = 16 if prec == "fp32" else 32                       # P + R + M per time index
+    plan = det.plan()
+    stored = int(torch.clamp(det.result.n_events, max=4).sum().item())
+    kern = {10: "aa_fast_kernel (register-staged)", 11: "aa_stream_kernel (streaming)",
+            30: "aa_exact_kernel<C128> (fp64 wave per stream)"}.get(plan // 100, "general engine")
+    return dict(config=name, workload=workload, kernel=f"{kern}, plan {plan}", samples=B * na * T, ms=ms,
+                alg_bytes=B * T * (na * esz + osz) + B * 4 + stored * 64,
+                bytes_per_sample=f"{na} x {esz} in + P/R/M {osz} per time index + events")
+
+
+def cfg3_T4096(dev, st, steps, warmup):
+    """SURVEY §8d sensitivity run: cfg3 with T = 4096 (65536 x 4096 c64, L = 512, fp32)."""
+    return _aa_cfg(dev, st, steps, warmup, "cfg3_T4096", 65536, 1, 4096, 512, torch.complex64, "fp32",
+                   "sync_aa S&C fp32 L=512, 65536 x 4096 c64 (T=4096 sensitivity)", 41)
+
+
+def aa_refshape_c64(dev, st, steps, warmup):
+    """The reference's own detector input shape (sync_aa.run_single_test, preamble 1024 + cir1:
+    2 antennas x 5315 samples, sync_aa.py:699-738), batched 16384 streams, c64 / fp32."""
+    return _aa_cfg(dev, st, steps, warmup, "aa_refshape_c64", 16384, 2, 5315, 512, torch.complex64, "fp32",
+                   "sync_aa S&C fp32 L=512, 16384 x 2 ant x 5315 c64 (reference run_single_test shape)", 43)
+
+
+def aa_refshape_c128(dev, st, steps, warmup):
+    """As aa_refshape_c64 in the reference's float64 (complex128 in, fp64 out)."""
+    return _aa_cfg(dev, st, steps, warmup, "aa_refshape_c128", 16384, 2, 5315, 512, torch.complex128, "fp64",
+                   "sync_aa S&C fp64 L=512, 16384 x 2 ant x 5315 c128 (reference run_single_test shape)", 43)
+
+
+CONFIGS = {"cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
+"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
 def main():

@@ -1,0 +1,82 @@
+"""Paired A/B of libofdmsync.so variants (tools/variants.py) on the same device buffers: the
+sync_aa detector (ofs_aa_detect) on one shape, lib order rotated every round.  Diagnostic only.
+
+    python tools/lib_ab.py --libs build/libofdmsync_a.so,build/libofdmsync_b.so --B 65536 --T 4096 --L 512 --na 1
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
+
+import torch  # noqa: E402
+
+from ofdm_sync_amd import _lib, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", required=True)
+    ap.add_argument("--B", type=int, default=65536)
+    ap.add_argument("--T", type=int, default=4096)
+    ap.add_argument("--L", type=int, default=512)
+    ap.add_argument("--na", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--detect-only", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, T, L, na, E = a.B, a.T, a.L, a.na, 4
+    base = synth.faded_base(L, "cir1", tuple(range(na)) if na > 1 else (1,))
+    x = synth.synth_batch(base, B, T, seed=5, device=dev)
+    P = None if a.detect_only else torch.empty((B, T), dtype=torch.complex64, device=dev)
+    R = None if a.detect_only else torch.empty((B, T), dtype=torch.float32, device=dev)
+    M = None if a.detect_only else torch.empty((B, T), dtype=torch.float32, device=dev)
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    libs = []
+    for p in a.libs.split(","):
+        l = ctypes.CDLL(os.path.abspath(p))
+        _lib._declare(l)
+        libs.append((os.path.basename(p), l))
+    args = (_lib.C64, x.data_ptr(), B, na, T, L, _lib.FP32, _lib.ptr(P), _lib.ptr(R), _lib.ptr(M), None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+    times = {n: [] for n, _ in libs}
+    ref = None
+    for r in range(a.rounds):
+        order = libs[r % len(libs):] + libs[:r % len(libs)]
+        for name, l in order:
+            for _ in range(3):
+                assert l.ofs_aa_detect(*args) == 0
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.steps):
+                l.ofs_aa_detect(*args)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / a.steps)
+            if ref is None:
+                ref = (n_ev.clone(), None if M is None else M.clone())
+            else:
+                assert torch.equal(ref[0], n_ev), f"{name}: events differ"
+                if M is not None:
+                    assert torch.equal(ref[1], M), f"{name}: M differs"
+    alg = B * T * (na * 8 + (0 if a.detect_only else 16))
+    for name, _ in libs:
+        ms = statistics.median(times[name])
+        print(json.dumps(dict(lib=name, shape=[B, na, T, L], plan=libs[0][1].ofs_aa_plan(_lib.C64, _lib.FP32, na, T, L),
+                              ms_median=round(ms, 4), ms_all=[round(t, 4) for t in times[name]],
+                              frac=round(alg / (ms / 1e3) / 8e12, 4))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
