@@ -277,41 +277,47 @@ constexpr int STREAM_WG = OFS_STREAM_WG;
 #define OFS_STREAM_BOUNDS __launch_bounds__(STREAM_WG)
 #endif
 
-template <int E, int MR, int NA, bool DO>
-__global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
-    constexpr int RL = 64 * E;
-    constexpr int L = MR * RL;
-    constexpr int V4 = E / 2;                                // sample pairs per lane per row
-    constexpr int PD = OFS_STREAM_PD > 0 ? OFS_STREAM_PD : (E == 2 ? 4 : 2);   // rows in flight ahead of use
-    constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
-    const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)xcd_block() * (STREAM_WG / 64) + (threadIdx.x >> 6);
-    if (b >= a.B) return;
-    const int64_t T = a.T;
-    const int Ti = (int)T;
-    const int nrows = (int)((T + RL - 1) / RL);
-    const int full_rows = (int)(T / RL);                     // rows entirely inside the stream
-    const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NA * T;
+#ifndef OFS_STREAM_FF
+#define OFS_STREAM_FF 1
+#endif
+// lag ring (raw samples of rows k-MR..k-1) in a wave-private LDS slice instead of VGPRs:
+// 0 = never, 1 = two antennas (frees 32 VGPRs there), 2 = always
+#ifndef OFS_STREAM_LDSLAG
+#define OFS_STREAM_LDSLAG 1
+#endif
 
-    float lr[NA][MR][E], li[NA][MR][E];                      // x of rows k-MR..k-1 (lag L)
+// per-wave state of the streaming kernel; row<U, FIRST, GUARD>() processes row k whose ring
+// position k mod PER == U is a compile-time constant: FIRST = rows k < MR (no lagged product,
+// window clipped at 0), GUARD = a row that may reach past T (partial row / tail)
+template <int E, int MR, int NA, bool DO>
+struct AaStream {
+    static constexpr int RL = 64 * E;
+    static constexpr int L = MR * RL;
+    static constexpr int V4 = E / 2;                         // sample pairs per lane per row
+    // rows in flight ahead of use (paired A/B, tools/lib_ab.py, r02e: 1 antenna PD 2, 2 antennas
+    // with the LDS lag ring PD 4; the peeled steady loop + scan-free gate flags + these took the
+    // T = 4096 shape 1.32 -> 1.09 ms and the 2 x 5315 reference shape 0.75 -> 0.49 ms)
+    static constexpr int PD = OFS_STREAM_PD > 0 ? OFS_STREAM_PD : ((E == 2 && NA == 2) ? 4 : 2);
+    static constexpr int PER = MR > PD ? MR : PD;            // unroll period (MR, PD powers of 2)
+    static constexpr bool LDSLAG = OFS_STREAM_LDSLAG == 2 || (OFS_STREAM_LDSLAG == 1 && NA == 2);
+
+    const float2* xb;
+    float4 (*lag)[NA][V4][64];                               // LDSLAG: [MR][NA][V4][lane]
+    int64_t T, o0;
+    int Ti, nrows, full_rows, lane;
+    float lr[LDSLAG ? 1 : NA][MR][E], li[LDSLAG ? 1 : NA][MR][E];   // x of rows k-MR..k-1 (lag L)
     float sR[MR][E], sI[MR][E], sE[MR][E];                   // retained in-window suffixes
     double cbR[MR], cbI[MR], cbE[MR];                        // row bases C[j], j in (k-MR, k]
-    double CR = 0.0, CI = 0.0, CE = 0.0;                     // C[k]: prefix at the start of row k
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-        cbR[m] = 0.0; cbI[m] = 0.0; cbE[m] = 0.0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f;
-#pragma unroll
-            for (int t = 0; t < NA; ++t) { lr[t][m][e] = 0.f; li[t][m][e] = 0.f; }
-        }
-    }
+    double CR, CI, CE;                                       // C[k]: prefix at the start of row k
+    float2 nx[PD][NA][E];                                    // rows k..k+PD-1 in flight
+    AaRowGate<E, float, false, (bool)(DO || OFS_STREAM_FF)> gate;
+    float2* Pout; float* Rout; float* Mout; uint8_t* Vout;
+    bool detect;
+    float floor_;
 
-    // a row's samples of one antenna: pairs as 8-byte-aligned float4 for whole rows, else
-    // per-sample with zero fill past T
-    float2 nx[PD][NA][E];
-    auto load_row = [&](int k, float2 (&dst)[NA][E]) {
+    // a row's samples of every antenna: 8-byte-aligned pair loads for whole rows, per-sample
+    // with zero fill past T otherwise (wave-uniform choice)
+    __device__ __forceinline__ void load_row(int k, float2 (&dst)[NA][E]) {
         const int64_t n0 = (int64_t)RL * k + E * lane;
 #pragma unroll
         for (int t = 0; t < NA; ++t) {
@@ -328,111 +334,179 @@ __global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
                 for (int e = 0; e < E; ++e) dst[t][e] = (n0 + e < T) ? xs[n0 + e] : make_float2(0.f, 0.f);
             }
         }
-    };
-#pragma unroll
-    for (int p = 0; p < PD; ++p)
-        if (p < nrows) load_row(p, nx[p]);
+    }
 
-    AaRowGate<E, float, false, DO> gate;
-    if (a.detect)
-        gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
-                  a.ev_r + b * (int64_t)a.max_ev * 4);
-    float2* Pout = DO ? nullptr : reinterpret_cast<float2*>(a.P);
-    float* Rout = DO ? nullptr : reinterpret_cast<float*>(a.R);
-    float* Mout = DO ? nullptr : reinterpret_cast<float*>(a.M);
-    uint8_t* Vout = DO ? nullptr : a.valid;
-    const float floor_ = 1e-6f * (float)L;
-
-    for (int k0 = 0; k0 < nrows; k0 += PER) {
+    template <int U, bool FIRST, bool GUARD>
+    __device__ __forceinline__ void row(int k) {
+        constexpr int sl = U % MR;                           // ring slot of row k-MR (and k)
+        constexpr int so = (U + 1) % MR;                     // slot of C[k-MR+1]
+        const int nb = RL * k + E * lane;
+        float2 cur[NA][E];
 #pragma unroll
-        for (int u = 0; u < PER; ++u) {
-            const int k = k0 + u;
-            if (k < nrows) {
-                const int nb = RL * k + E * lane;
-                const int sl = u % MR;                       // ring slot of row k-MR (and k)
-                float2 cur[NA][E];
+        for (int t = 0; t < NA; ++t)
 #pragma unroll
-                for (int t = 0; t < NA; ++t)
+            for (int e = 0; e < E; ++e) cur[t][e] = nx[U % PD][t][e];
+        if (!GUARD || k + PD < nrows) load_row(k + PD, nx[U % PD]);
+        // lagged samples x[n-L] (row k-MR) of every antenna
+        float dr[NA][E], di[NA][E];
 #pragma unroll
-                    for (int e = 0; e < E; ++e) cur[t][e] = nx[u % PD][t][e];
-                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
-                // ---- lagged products x[n]·conj(x[n-L]) and energies, summed over the antennas ----
-                float aR[E], aI[E], aE[E];
+        for (int t = 0; t < NA; ++t) {
+            if constexpr (LDSLAG) {
 #pragma unroll
-                for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
-#pragma unroll
-                for (int t = 0; t < NA; ++t)
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const float cr = cur[t][e].x, ci = cur[t][e].y;
-                        aE[e] += fmaf(cr, cr, ci * ci);
-                        if (k >= MR) {
-                            aR[e] += fmaf(cr, lr[t][sl][e], ci * li[t][sl][e]);
-                            aI[e] += fmaf(ci, lr[t][sl][e], -(cr * li[t][sl][e]));
-                        }
-                        lr[t][sl][e] = cr; li[t][sl][e] = ci;
-                    }
-                // ---- in-lane partials (forward f, backward g), fp64 wave scan ----
-                float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
-                fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
-#pragma unroll
-                for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
-                gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
-#pragma unroll
-                for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
-                const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
-                const double tR = readlane(iR, 63), tI = readlane(iI, 63), tE = readlane(iE, 63);
-                const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);
-                const float uR = (float)(tR - iR), uI = (float)(tI - iI), uE = (float)(tE - iE);
-                const int so = (u + 1) % MR;                 // slot of C[k-MR+1]
-                const float wR = (float)(k >= MR ? CR - cbR[so] : CR);
-                const float wI = (float)(k >= MR ? CI - cbI[so] : CI);
-                const float wE = (float)(k >= MR ? CE - cbE[so] : CE);
-                // ---- window sums P = suffix(row k-MR) + rows between + prefix(row k) ----
-                float pr[E], pi[E], rf[E], mf[E], pmf[E];
+                for (int j = 0; j < V4; ++j) {
+                    const float4 v = FIRST ? make_float4(0.f, 0.f, 0.f, 0.f) : lag[sl][t][j][lane];
+                    dr[t][2 * j] = v.x; di[t][2 * j] = v.y; dr[t][2 * j + 1] = v.z; di[t][2 * j + 1] = v.w;
+                    lag[sl][t][j][lane] = make_float4(cur[t][2 * j].x, cur[t][2 * j].y, cur[t][2 * j + 1].x,
+                                                      cur[t][2 * j + 1].y);
+                }
+            } else {
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    float PR = wR + (xR + fR[e]), PI = wI + (xI + fI[e]), RR = wE + (xE + fE[e]);
-                    if (k >= MR) { PR += sR[sl][e]; PI += sI[sl][e]; RR += sE[sl][e]; }
-                    sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
-                    const float pm = fmaf(PR, PR, PI * PI);
-                    float m = 0.f;
-                    if (k >= MR && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
-                    pr[e] = PR; pi[e] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
+                    dr[t][e] = lr[t][sl][e]; di[t][e] = li[t][sl][e];
+                    lr[t][sl][e] = cur[t][e].x; li[t][sl][e] = cur[t][e].y;
                 }
-                cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
-                CR += tR; CI += tI; CE += tE;
-                // ---- stores ----
-                if (!DO) {
-                    const int64_t o = b * T + nb;
-                    if (k < full_rows) {
+            }
+        }
+        // ---- lagged products x[n]·conj(x[n-L]) and energies, summed over the antennas ----
+        float aR[E], aI[E], aE[E];
 #pragma unroll
-                        for (int j = 0; j < V4; ++j) {
-                            if (Pout) *reinterpret_cast<f4u*>(Pout + o + 2 * j) = f4u{pr[2 * j], pi[2 * j], pr[2 * j + 1], pi[2 * j + 1]};
-                            if (Rout) *reinterpret_cast<f2u*>(Rout + o + 2 * j) = f2u{rf[2 * j], rf[2 * j + 1]};
-                            if (Mout) *reinterpret_cast<f2u*>(Mout + o + 2 * j) = f2u{mf[2 * j], mf[2 * j + 1]};
-                        }
-                    } else {
+        for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
 #pragma unroll
-                        for (int e = 0; e < E; ++e)
-                            if (nb + e < Ti) {
-                                if (Pout) Pout[o + e] = make_float2(pr[e], pi[e]);
-                                if (Rout) Rout[o + e] = rf[e];
-                                if (Mout) Mout[o + e] = mf[e];
-                            }
-                    }
-                    if (Vout) {
+        for (int t = 0; t < NA; ++t)
 #pragma unroll
-                        for (int e = 0; e < E; ++e)
-                            if (nb + e < Ti) Vout[o + e] = (uint8_t)(k >= MR);
-                    }
+            for (int e = 0; e < E; ++e) {
+                const float cr = cur[t][e].x, ci = cur[t][e].y;
+                aE[e] += fmaf(cr, cr, ci * ci);
+                if (!FIRST) {
+                    aR[e] += fmaf(cr, dr[t][e], ci * di[t][e]);
+                    aI[e] += fmaf(ci, dr[t][e], -(cr * di[t][e]));
                 }
-                // ---- events: closed-form gate machine, streamed per row (aa_gate.h) ----
-                if (a.detect && k >= MR) gate.row(lane, k, nb, Ti, mf, pmf, pr, pi);
+            }
+        // ---- in-lane partials (forward f, backward g), fp64 wave scan ----
+        float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
+        fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
+        gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+#pragma unroll
+        for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+        const double iE = scan_add((double)fE[E - 1]);
+        const double tE = readlane(iE, 63);
+        const float xE = (float)shr1z(iE), uE = (float)(tE - iE);
+        double iR = 0.0, iI = 0.0, tR = 0.0, tI = 0.0;
+        float xR = 0.f, xI = 0.f, uR = 0.f, uI = 0.f;
+        if (!FIRST) {                                        // no lagged product before row MR
+            iR = scan_add((double)fR[E - 1]); iI = scan_add((double)fI[E - 1]);
+            tR = readlane(iR, 63); tI = readlane(iI, 63);
+            xR = (float)shr1z(iR); xI = (float)shr1z(iI);
+            uR = (float)(tR - iR); uI = (float)(tI - iI);
+        }
+        const float wR = (float)(FIRST ? CR : CR - cbR[so]);
+        const float wI = (float)(FIRST ? CI : CI - cbI[so]);
+        const float wE = (float)(FIRST ? CE : CE - cbE[so]);
+        // ---- window sums P = suffix(row k-MR) + rows between + prefix(row k) ----
+        float pr[E], pi[E], rf[E], mf[E], pmf[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            float PR = wR + (xR + fR[e]), PI = wI + (xI + fI[e]), RR = wE + (xE + fE[e]);
+            if (!FIRST) { PR += sR[sl][e]; PI += sI[sl][e]; RR += sE[sl][e]; }
+            sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
+            const float pm = fmaf(PR, PR, PI * PI);
+            float m = 0.f;
+            if (!FIRST && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
+            pr[e] = PR; pi[e] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
+        }
+        cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
+        CR += tR; CI += tI; CE += tE;
+        // ---- stores ----
+        if (!DO) {
+            const int64_t o = o0 + nb;
+            if (!GUARD || k < full_rows) {
+#pragma unroll
+                for (int j = 0; j < V4; ++j) {
+                    if (Pout) *reinterpret_cast<f4u*>(Pout + o + 2 * j) = f4u{pr[2 * j], pi[2 * j], pr[2 * j + 1], pi[2 * j + 1]};
+                    if (Rout) *reinterpret_cast<f2u*>(Rout + o + 2 * j) = f2u{rf[2 * j], rf[2 * j + 1]};
+                    if (Mout) *reinterpret_cast<f2u*>(Mout + o + 2 * j) = f2u{mf[2 * j], mf[2 * j + 1]};
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (nb + e < Ti) {
+                        if (Pout) Pout[o + e] = make_float2(pr[e], pi[e]);
+                        if (Rout) Rout[o + e] = rf[e];
+                        if (Mout) Mout[o + e] = mf[e];
+                    }
+            }
+            if (Vout) {
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (nb + e < Ti) Vout[o + e] = (uint8_t)(!FIRST);
+            }
+        }
+        // ---- events: closed-form gate machine, streamed per row (aa_gate.h) ----
+        if (!FIRST && detect) gate.row(lane, k, nb, Ti, mf, pmf, pr, pi);
+    }
+
+    // rows [k0, k0 + PER) with k0 % PER == 0; FIRST_BLOCK: k0 == 0 (rows < MR are FIRST)
+    template <bool FIRST_BLOCK, bool GUARD, int U = 0>
+    __device__ __forceinline__ void block(int k0) {
+        if constexpr (U < PER) {
+            const int k = k0 + U;
+            if (!GUARD || k < nrows) {
+                row<U, FIRST_BLOCK && (U < MR), GUARD>(k);
+                block<FIRST_BLOCK, GUARD, U + 1>(k0);
             }
         }
     }
-    if (a.detect) gate.finish(lane, Ti, a.n_ev + b);
+};
+
+template <int E, int MR, int NA, bool DO>
+__global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
+    using S = AaStream<E, MR, NA, DO>;
+    __shared__ float4 lagbuf[STREAM_WG / 64][S::LDSLAG ? MR : 1][NA][S::V4][64];
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)xcd_block() * (STREAM_WG / 64) + (threadIdx.x >> 6);
+    if (b >= a.B) return;
+    S s;
+    s.lane = lane;
+    s.lag = lagbuf[threadIdx.x >> 6];
+    s.T = a.T;
+    s.Ti = (int)a.T;
+    s.o0 = b * a.T;
+    s.nrows = (int)((a.T + S::RL - 1) / S::RL);
+    s.full_rows = (int)(a.T / S::RL);                        // rows entirely inside the stream
+    s.xb = reinterpret_cast<const float2*>(a.x) + b * NA * a.T;
+    s.CR = s.CI = s.CE = 0.0;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        s.cbR[m] = 0.0; s.cbI[m] = 0.0; s.cbE[m] = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            s.sR[m][e] = 0.f; s.sI[m][e] = 0.f; s.sE[m][e] = 0.f;
+#pragma unroll
+            for (int t = 0; t < (S::LDSLAG ? 1 : NA); ++t) { s.lr[t][m][e] = 0.f; s.li[t][m][e] = 0.f; }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < S::PD; ++p)
+        if (p < s.nrows) s.load_row(p, s.nx[p]);
+    s.detect = a.detect != 0;
+    if (s.detect)
+        s.gate.init(a.hyst, S::L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
+                    a.ev_r + b * (int64_t)a.max_ev * 4);
+    s.Pout = DO ? nullptr : reinterpret_cast<float2*>(a.P);
+    s.Rout = DO ? nullptr : reinterpret_cast<float*>(a.R);
+    s.Mout = DO ? nullptr : reinterpret_cast<float*>(a.M);
+    s.Vout = DO ? nullptr : a.valid;
+    s.floor_ = 1e-6f * (float)S::L;
+
+    // warm-up block (rows 0..PER-1: the first MR have no lagged product), steady blocks of
+    // whole rows with no per-row guards, then the guarded tail
+    s.template block<true, true>(0);
+    int k0 = S::PER;
+    for (; k0 + S::PER + S::PD <= s.full_rows; k0 += S::PER) s.template block<false, false>(k0);
+    for (; k0 < s.nrows; k0 += S::PER) s.template block<false, true>(k0);
+    if (a.detect) s.gate.finish(lane, s.Ti, a.n_ev + b);
 }
 
 template <int E, int MR, int NA>
