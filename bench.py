@@ -79,15 +79,16 @@ def _free_port() -> int:
     return p
 
 
-def launch_ranks(a, argv) -> int:
-    """Start N ranks under torch.distributed.run as a child process (nothing here has touched
-    the GPU; torch.cuda.device_count() does not initialise it on this image)."""
+def launch_ranks(a, argv, script: str | None = None) -> int:
+    """Start N ranks of `script` (default: this file) under torch.distributed.run as a child
+    process (nothing here has touched the GPU; torch.cuda.device_count() does not initialise
+    it on this image)."""
     if not a.selftest_cpu:
         n = torch.cuda.device_count()
         if n < a.gpus:
             raise SystemExit(f"bench.py --gpus {a.gpus}: only {n} GPU(s) visible")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), script or os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "1")
@@ -129,7 +130,8 @@ def _pool_leg(xh, L, form, workers, budget):
              "loop": "literal per-sample Python loop (ofdm_oracle.aa_detect_loop: the reference's "
                      "DelayLine/RunningSum streaming form, sync_aa.py:458-568)"}[form]
     return dict(value=r["value"], unit="Msamples/s", cores=workers, kind="port",
-                sample=f"{r['streams']} streams x {r['T']} c64 of the same batch, L={L}, {label}, "
+                sample=f"{r['streams']} stream runs x {r['T']} c64 (cycling over {n} streams of the same batch), "
+                       f"L={L}, {label}, "
                        f"pool of {workers} processes, {r['seconds']:.2f} s wall")
 
 

@@ -9,7 +9,7 @@ the product.
 Runs ``ofdm_oracle.aa_detect`` (vectorised prefix sums + the reference's gate loop) or
 ``ofdm_oracle.aa_detect_loop`` (the reference's per-sample streaming loop, sync_aa.py:458-568)
 over the streams of x[B, n_ant, T], one stream per task, on a pool of `workers` processes,
-until ~budget_s of wall time; prints one JSON line with the rate.
+until ~budget_s of wall time (cycling over the streams); prints one JSON line with the rate.
 """
 from __future__ import annotations
 
@@ -48,10 +48,9 @@ def main():
         pool.map(_one, [(b % B, L, form) for b in range(workers)])          # warm every worker
         done, t0, b = 0, time.perf_counter(), 0
         chunk = workers * (1 if form == "loop" else 8)
-        while time.perf_counter() - t0 < budget and b < B:
-            n = min(chunk, B - b)
-            done += sum(pool.map(_one, [(i, L, form) for i in range(b, b + n)]))
-            b += n
+        while time.perf_counter() - t0 < budget and b < 64 * B:   # the sample cycles over the streams
+            done += sum(pool.map(_one, [(i % B, L, form) for i in range(b, b + chunk)]))
+            b += chunk
         dt = time.perf_counter() - t0
     print(json.dumps(dict(value=done / dt / 1e6, streams=b, samples=done, seconds=dt, workers=workers,
                           form=form, T=T)))

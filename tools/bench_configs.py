@@ -1,4 +1,4 @@
-"""Secondary BASELINE.json configurations (cfg2, cfg4, cfg5) on one GPU.
+"""Secondary BASELINE.json configurations (cfg2, cfg4, cfg5, ...), one GPU or N.
 
 bench.py measures the headline (cfg3).  This script times the other configs named in
 BASELINE.json with the same method (warm-up, then K launches bracketed by HIP events on the
@@ -6,7 +6,15 @@ launch stream, inputs resident in HBM) and prints one JSON line per config with 
 algorithmic bytes per launch and the achieved fraction of the
 8 TB/s HBM peak.  Synthetic inputs of the config's shape; not the driver's headline line.
 
-    python tools/bench_configs.py [--configs cfg2a,cfg2b,cfg4,cfg5] [--steps K] [--warmup W]
+Multi-GPU (BASELINE configs[3] "262144 streams sharded across 8 x MI355X", configs[4] "1M
+sequences, 1 -> 8 GPU scaling"): ``--gpus N`` starts N ranks (torch.distributed.run child,
+as bench.py); cfg4 / cfg5 / cfg5_rocfft are STRONG-scaled: the fixed global batch
+(--cfg4-global, --cfg5-global) is split by shard.shard_bounds, each rank runs its shard with
+no data-path collective, the timed region is bracketed by a barrier and the reported time is
+the MAX over ranks; value = global samples / that time.  The other configs run per rank
+(weak) and are reported by rank 0.
+
+    python tools/bench_configs.py [--configs cfg2a,cfg2b,cfg4,cfg5] [--steps K] [--warmup W] [--gpus N]
 """
 from __future__ import annotations
 
@@ -22,15 +30,19 @@ sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from ofdm_sync_amd import _lib, synth, zc_freq  # noqa: E402
+from ofdm_sync_amd import _lib, shard, synth, zc_freq  # noqa: E402
 
 HBM = 8000.0
+_DIST = None                     # torch.distributed when run with N ranks (barrier before timing)
 
 
 def timed(step, steps, warmup, stream):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if _DIST is not None:
+        _DIST.barrier()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(steps):
@@ -138,10 +150,11 @@ def cfg2b(dev, st, steps, warmup):
                 bytes_per_sample="4 in + 6 x f64 8 + 2 flags")
 
 
-def cfg4(dev, st, steps, warmup):
-    """cfg4 per-GPU shard: combined S&C (both-halves R) + Minn, N=2048, 32768 x 4096 c64, fp32."""
-    B, T, N = 32768, 4096, 2048
-    x = dput(dev, synth.make_aa_batch(B, T, N // 2, seed=4, device=dev))
+def cfg4(dev, st, steps, warmup, B=32768, seed=4):
+    """cfg4: combined S&C (both-halves R) + Minn, N=2048, B x 4096 c64, fp32 (B = this rank's
+    shard of the global 262144 streams)."""
+    T, N = 4096, 2048
+    x = dput(dev, synth.make_aa_batch(B, T, N // 2, seed=seed, device=dev))
     n_out = T - N + 1
     outs = [dbuf(dev, (B, n_out), dt) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
     L_ = _lib.lib()
@@ -165,10 +178,11 @@ def cfg4(dev, st, steps, warmup):
                 alg_bytes=nbytes, bytes_per_sample="8 in (once) + 2 x (M 4 + P 8 + R 4) per output")
 
 
-def cfg5(dev, st, steps, warmup, n_seq=1 << 20):
-    """cfg5: zc_freq metric, N=4096, one window per sequence (cp=0), 1M sequences x 4096 c64."""
+def cfg5(dev, st, steps, warmup, n_seq=1 << 20, seed=5):
+    """cfg5: zc_freq metric, N=4096, one window per sequence (cp=0), n_seq sequences x 4096 c64
+    (n_seq = this rank's shard of the global 1M)."""
     N = 4096
-    g = torch.Generator(device=dev).manual_seed(5)
+    g = torch.Generator(device=dev).manual_seed(seed)
     prec = int(os.environ.get("OFS_CFG5_PREC", "0"))           # 0 fp32 window FFT, 1 fp64 sliding DFT
     x, out = batch_arena(dev, [((n_seq, N), torch.complex64),
                                ((n_seq, 1), torch.float32 if prec == 0 else torch.float64)], contiguous=True)
@@ -281,7 +295,7 @@ def cfg3_fp64(dev, st, steps, warmup):
                 bytes_per_sample="16 in + P 16 + R 8 + M 8")
 
 
-def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20):
+def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5):
     """cfg5 through the rocFFT leg (ofs_zc_freq_metric_fft: batched rocFFT of every window into a
     dense spectrum, then the HIP gather/metric kernel and the per-sequence argmax), same input as
     cfg5.  alg_bytes counts the same 8 B/sample + output as cfg5 so Msamples/s and frac compare
@@ -404,24 +418,67 @@ CONFIGS = {"cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_ref
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
-def main():
+# strong-scaled configs: global batch and the keyword that receives the rank's shard
+SHARDED = {"cfg4": ("cfg4_global", "B"), "cfg5": ("cfg5_global", "n_seq"), "cfg5_rocfft": ("cfg5_global", "n_seq")}
+
+
+def main(argv=None):
+    global _DIST
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default=",".join(CONFIGS))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    a = ap.parse_args()
-    dev = torch.device("cuda", 0)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--cfg4-global", type=int, default=262144, help="cfg4 streams over all GPUs")
+    ap.add_argument("--cfg5-global", type=int, default=1 << 20, help="cfg5 sequences over all GPUs")
+    a = ap.parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.path.insert(0, ROOT)
+        import bench
+        return bench.launch_ranks(argparse.Namespace(gpus=a.gpus, selftest_cpu=False), argv,
+                                  script=os.path.abspath(__file__))
+    info = shard.rank_info()
+    if info.world != a.gpus:
+        raise SystemExit(f"bench_configs.py: --gpus {a.gpus} but WORLD_SIZE={info.world}")
+    torch.cuda.set_device(info.local_rank)
+    dev = torch.device("cuda", info.local_rank)
+    _DIST = shard.init("nccl", dev)
     st = torch.cuda.current_stream(dev)
     for name in a.configs.split(","):
         t0 = time.perf_counter()
-        r = CONFIGS[name](dev, st, a.steps, a.warmup)
-        gbs = r["alg_bytes"] / (r["ms"] / 1e3) / 1e9
-        r.update(value=round(r["samples"] / (r["ms"] / 1e3) / 1e6, 1), unit="Msamples/s",
-                 ms=round(r["ms"], 4), achieved_GBs=round(gbs, 1), hbm_frac=round(gbs / HBM, 4),
+        kw, scale = {}, 1
+        if name in SHARDED:
+            gkey, arg = SHARDED[name]
+            total = getattr(a, gkey)
+            lo, hi = shard.shard_bounds(total, info.rank, info.world)
+            kw = {arg: hi - lo, "seed": shard.shard_seed(5, info.rank)}
+        r = CONFIGS[name](dev, st, a.steps, a.warmup, **kw)
+        ms_rank = r["ms"]
+        ms = shard.max_over_ranks(ms_rank, _DIST, dev)
+        if name in SHARDED:
+            # global samples: every rank's shard (sum); alg bytes likewise
+            tot = torch.tensor([r["samples"], r["alg_bytes"]], dtype=torch.float64, device=dev)
+            if _DIST is not None:
+                _DIST.all_reduce(tot)
+            r["samples"], r["alg_bytes"] = int(tot[0].item()), int(tot[1].item())
+            r.update(scaling="strong", global_batch=getattr(a, SHARDED[name][0]), n_gpus=info.world,
+                     shard=[lo, hi], rank_ms=round(ms_rank, 4))
+        else:
+            r.update(scaling="per-rank", n_gpus=info.world)
+        r["ms"] = ms
+        gbs = r["alg_bytes"] / (ms / 1e3) / 1e9
+        r.update(value=round(r["samples"] / (ms / 1e3) / 1e6, 1), unit="Msamples/s",
+                 ms=round(ms, 4), achieved_GBs=round(gbs, 1),
+                 hbm_frac=round(gbs / (HBM * (info.world if name in SHARDED else 1)), 4),
                  wall_s=round(time.perf_counter() - t0, 1))
-        print(json.dumps(r), flush=True)
+        if info.rank == 0:
+            print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
+    if _DIST is not None:
+        _DIST.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
