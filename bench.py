@@ -242,7 +242,7 @@ def main(argv=None):
         det = sync_aa.AABatchDetector(B, T, 1, L, precision="fp32", outputs=("P", "R", "M"), max_events=E,
                                       placement=a.placement, device=dev)
         # synthetic shard: per-rank seed = the stream range it owns (weak: fresh streams per rank)
-        det.x.copy_(synth.make_aa_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev))
+        det.x.copy_(synth.headline_batch(B, T, L, seed=shard.shard_seed(2026, rank), device=dev))
         torch.cuda.empty_cache()
         stream = torch.cuda.current_stream(dev)
         step = det.run
@@ -285,8 +285,9 @@ def main(argv=None):
         "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": "f32 (c64 in, f64 prefix sums)",
-        "data": "synthetic (ofs_synth_batch on the GPU): [A][A] ZC preamble (sync_aa.build_aa_preamble "
-                "restated) * cir1 ch1 + AWGN U[0,15] dB + CFO U[-5,5] kHz @ 15.36 MHz, random window offset",
+        "data": "synthetic (ofs_synth_frames on the GPU): per-stream sync_aa.run_single_test frames - [A][A] "
+                "ZC preamble + own random-QPSK pilot/data symbols, * cir1 RX ch1 (1100 taps) + AWGN U[0,15] dB + "
+                "CFO U[-5,5] kHz @ 15.36 MHz; 1024-sample window at a random offset around the preamble",
         "config": {"workload": "cfg3 Schmidl-Cox float32 metric+CFO, N=1024 (L=512), cir1, "
                                f"{B} streams x {T} c64 per GPU",
                    "global_batch": B_glob, "seq_len": T, "L": L,

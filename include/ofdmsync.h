@@ -238,6 +238,31 @@ int32_t ofs_synth_batch(const void* base, int64_t base_len, int32_t n_br, int64_
                         double adc_scale, void* out, double* params, void* stream);
 
 /*
+ * Frame synthesis: the whole per-stream chain of sync_aa.run_single_test (sync_aa.py:699-738),
+ * every stream its own frame and payload:
+ *   frame_b = [pre_pad zeros][preamble][n_sym random-QPSK OFDM symbols + CP][post_pad zeros]
+ *             (symbols as sync_aa.build_random_qpsk_symbol, sync_aa.py:238-260: QPSK on the n_bins
+ *             FFT bins `bins` (centred index k -> k mod n_fft), inverse FFT, unit power, CP);
+ *   y_br     = frame_b conv cir_br (sync_aa.py:611-621); rx_br = (y_br + CN(0, mean|y_br|^2 /
+ *             10^(snr_b/10))) * exp(i 2 pi cfo_b n / fs) (:622-631, :637-645);
+ *   if full_scale_ratio > 0: quantize_adc(rx, rms(rx over all branches) * full_scale_ratio)
+ *             (:263-291, :726-735), 12 bits;
+ *   out[b][br][t] = rx_br[win_start + off_b + t] (0 outside the frame), off_b ~ U{0..max_offset-1}.
+ *   preconv: [n_br][pre_len + taps - 1] c128 = preamble conv cir_br (shared part, host-built);
+ *   cir: [n_br][taps] c128; n_br <= 4; n_fft a power of two <= 4096.
+ *   out_fmt OFS_C64 | OFS_C128 (dequantized values if quantized) | OFS_CI16 (ADC codes when
+ *   quantized); params [B][4] f64 = window start, snr_db, cfo_hz, full scale (nullable);
+ *   phases [B][n_sym][n_bins] u8 = the QPSK phase indices drawn (nullable).
+ */
+int32_t ofs_synth_frames(const void* preconv, int64_t preconv_len, const void* cir, int64_t taps,
+                         int32_t n_br, int32_t pre_pad, int32_t pre_len, int32_t n_sym, int32_t n_fft,
+                         int32_t cp_len, const int32_t* bins, int32_t n_bins, int32_t post_pad, int64_t B,
+                         int64_t T, int64_t win_start, int32_t max_offset, double snr_lo_db,
+                         double snr_hi_db, double cfo_lo_hz, double cfo_hi_hz, double fs_hz,
+                         double full_scale_ratio, uint64_t seed, int32_t out_fmt, void* out,
+                         double* params, uint8_t* phases, void* stream);
+
+/*
  * Park mirror-symmetry metric: replaces park.park_streaming_metric (park.py:64-114).
  * half = N/2; outputs for d in [half, T-half-1], n_out = T - 2*half, laid out [B][n_out]:
  *   P (c64|c128) = sum_br sum_{k<half} x[d-k]*x[d+k]; E (f32|f64) = sum_br sum_{k<half}|x[d+k]|^2;

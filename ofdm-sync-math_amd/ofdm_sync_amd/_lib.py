@@ -73,6 +73,10 @@ def _declare(lib):
                                      P, c_int32, P, P, c_int64, P, c_int64, P, P, P, P, P, P, P, P, P]),
         "ofs_synth_batch": (c_int32, [P, c_int64, c_int32, c_int64, c_int64, c_int32, c_double, c_double, c_double,
                                       c_double, c_double, ctypes.c_uint64, c_int32, c_double, P, P, P]),
+        "ofs_synth_frames": (c_int32, [P, c_int64, P, c_int64, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                       c_int32, P, c_int32, c_int32, c_int64, c_int64, c_int64, c_int32,
+                                       c_double, c_double, c_double, c_double, c_double, c_double,
+                                       ctypes.c_uint64, c_int32, P, P, P, P]),
         "ofs_park_metric": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, P, P,
                                       P, P]),
         "ofs_zc_correlate": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_double,

@@ -1,11 +1,16 @@
 """Synthetic receive-stream batches for benchmarks and tests (input synthesis, not the hot path).
 
-Restates the reference's input builders closely enough to produce realistic streams:
+Restates the reference's input builders (pinned to the reference's own outputs in
+tests/test_host_logic.py against tests/golden/synth_builders.npz):
   aa_preamble      <- sync_aa.build_aa_preamble (sync_aa.py:160-235)
   load_cir         <- channel.load_measured_cir (channel.py:15-48)
-  make_aa_batch    <- run_single_test's channel + AWGN + CFO chain (sync_aa.py:577-645),
-  synth_batch         generated per stream on the GPU by ofs_synth_batch (csrc/synth.hip;
-                      Philox RNG: distribution-level parity with numpy).
+  qpsk_symbol      <- sync_aa.build_random_qpsk_symbol (sync_aa.py:238-260), draws given
+  frame            <- run_single_test's frame assembly (sync_aa.py:702-712)
+  frames_batch     <- the whole run_single_test chain per stream on the GPU (ofs_synth_frames:
+                      own QPSK payload per stream, CIR convolution, AWGN, CFO, 12-bit ADC)
+  make_aa_batch    <- a cheaper form for the headline batch: one faded preamble (preamble ⊛ CIR)
+  synth_batch         shifted per stream + CFO + AWGN (ofs_synth_batch).
+Philox RNG on the GPU: distribution-level parity with numpy.
 """
 from __future__ import annotations
 
@@ -51,6 +56,39 @@ def load_cir(name: str = "cir1") -> np.ndarray:
     for i, c in enumerate(chans):
         out[i, :len(c)] = c
     return out
+
+
+# frame geometry of sync_aa.run_single_test (sync_aa.py:99-125, :699-712)
+N_FFT = 1024
+CYCLIC_PREFIX = 72
+NUM_ACTIVE = 600
+PRE_PAD = 500
+POST_PAD = 500
+
+
+def active_bins(n_fft: int = N_FFT, num_active: int = NUM_ACTIVE) -> np.ndarray:
+    """FFT bins of the centred active subcarriers after ifftshift (sync_aa.py:131-145 + the
+    ifftshift of :247): centred index k -> bin k mod N."""
+    half = num_active // 2
+    k = np.concatenate([np.arange(-half, 0), np.arange(1, half + 1)])
+    return (k % n_fft).astype(np.int32)
+
+
+def qpsk_symbol(phases, n_fft: int = N_FFT, cp: int = CYCLIC_PREFIX) -> np.ndarray:
+    """Random-QPSK OFDM symbol with CP from its phase indices (0..3 per active subcarrier):
+    restates sync_aa.build_random_qpsk_symbol (sync_aa.py:238-260) with the draws given."""
+    phases = np.asarray(phases)
+    q = np.exp(1j * np.pi / 4 * (2 * phases + 1)) / np.sqrt(2)
+    spec = np.zeros(n_fft, complex)
+    spec[active_bins(n_fft, len(phases))] = q
+    sym = np.fft.ifft(spec) * np.sqrt(n_fft)
+    sym = sym / np.sqrt(np.mean(np.abs(sym) ** 2))
+    return np.concatenate([sym[-cp:], sym])
+
+
+def frame(preamble, symbols, pre_pad: int = PRE_PAD, post_pad: int = POST_PAD) -> np.ndarray:
+    """[pad][preamble][symbols...][pad] (sync_aa.py:705-712)."""
+    return np.concatenate([np.zeros(pre_pad, complex), preamble, *symbols, np.zeros(post_pad, complex)])
 
 
 def faded_base(L: int = 512, cir: str | None = "cir1", branches=(1,)) -> np.ndarray:
@@ -106,6 +144,73 @@ def make_aa_batch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, cir:
     """
     return synth_batch(faded_base(L, cir, (branch,)), B, T, max_offset=max_offset, snr_db=snr_db, cfo_hz=cfo_hz,
                        fs=fs, seed=seed, device=device, dtype=dtype)
+
+
+class Frames:
+    """Result of ``frames_batch``: x [B, n_br, T] (or [..., 2] int16 codes), params [B, 4] f64
+    (window start, snr_db, cfo_hz, full scale), phases [B, n_sym, n_bins] u8 (QPSK draws)."""
+
+    def __init__(self, x, params, phases, preamble, cir):
+        self.x, self.params, self.phases, self.preamble, self.cir = x, params, phases, preamble, cir
+
+
+def frames_batch(B: int, T: int | None = None, *, preamble_len: int = 1024, cir: str | None = "cir1",
+                 n_br: int = 2, branches=None, n_sym: int = 2, snr_db=(0.0, 15.0), cfo_hz=(-5000.0, 5000.0),
+                 fs: float = 15.36e6, full_scale_ratio: float | None = None, win_start: int = 0,
+                 max_offset: int = 1, seed: int = 2026, device="cuda", dtype=torch.complex64,
+                 return_phases: bool = False) -> Frames:
+    """ofs_synth_frames: B independent frames of sync_aa.run_single_test (sync_aa.py:699-738) -
+    [A][A] preamble + n_sym random-QPSK symbols (per stream) between 500-sample pads, per-branch
+    CIR convolution, AWGN at a per-stream SNR, CFO, optional 12-bit ADC (full_scale_ratio) -
+    generated on the GPU.  T defaults to the whole received frame (pads + preamble + symbols +
+    taps - 1); the window starts at win_start + U{0..max_offset-1}.  cir None: AWGN only
+    (a one-tap identity channel, as apply_channel_multi_antenna's channel_name=None).
+    ``branches``: CIR bank rows to use (default the first n_br, as the reference)."""
+    pre = aa_preamble(preamble_len)
+    if cir is None:
+        h = np.ones((n_br, 1), complex)
+    elif branches is not None:
+        h = load_cir(cir)[list(branches)]
+        n_br = h.shape[0]
+    else:
+        h = load_cir(cir)[:n_br]
+        if h.shape[0] < n_br:                                 # sync_aa.py:603-606: tile the bank
+            h = np.tile(h, (n_br // h.shape[0] + 1, 1))[:n_br]
+    pc = np.stack([np.convolve(pre, h[br]) for br in range(n_br)])
+    bins = active_bins()
+    Lout = PRE_PAD + preamble_len + n_sym * (N_FFT + CYCLIC_PREFIX) + POST_PAD + h.shape[1] - 1
+    T = Lout if T is None else int(T)
+    dev = torch.device(device)
+    if dtype not in _FMT:
+        raise TypeError(f"unsupported output dtype {dtype}")
+    shape = (B, n_br, T, 2) if dtype == torch.int16 else (B, n_br, T)
+    out = torch.empty(shape, dtype=dtype, device=dev)
+    params = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    phases = torch.empty((B, n_sym, len(bins)), dtype=torch.uint8, device=dev) if return_phases else None
+    pct = torch.from_numpy(np.ascontiguousarray(pc)).to(dev)
+    ht = torch.from_numpy(np.ascontiguousarray(h.astype(np.complex128))).to(dev)
+    bt = torch.from_numpy(bins).to(dev)
+    with torch.cuda.device(dev):
+        rc = _lib.lib().ofs_synth_frames(pct.data_ptr(), pc.shape[1], ht.data_ptr(), h.shape[1], n_br, PRE_PAD,
+                                         preamble_len, n_sym, N_FFT, CYCLIC_PREFIX, bt.data_ptr(), len(bins),
+                                         POST_PAD, B, T, int(win_start), int(max_offset), float(snr_db[0]),
+                                         float(snr_db[1]), float(cfo_hz[0]), float(cfo_hz[1]), float(fs),
+                                         float(full_scale_ratio or 0.0), int(seed) & ((1 << 64) - 1), _FMT[dtype],
+                                         out.data_ptr(), params.data_ptr(), _lib.ptr(phases),
+                                         torch.cuda.current_stream(dev).cuda_stream)
+    _lib.check(rc, "ofs_synth_frames")
+    torch.cuda.current_stream(dev).synchronize()             # host-built inputs are freed on return
+    return Frames(out, params, phases, pre, h)
+
+
+def headline_batch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, device="cuda",
+                   dtype=torch.complex64) -> torch.Tensor:
+    """The bench's cfg3 input: [B, 1, T] windows of per-stream run_single_test frames
+    ([A][A] preamble of 2L, own QPSK payload, cir1 RX branch 1, AWGN U[0, 15] dB, CFO U[-5, 5] kHz
+    at 15.36 MHz), each window starting U{0..127} samples before the preamble + 64."""
+    return frames_batch(B, T, preamble_len=2 * L, cir="cir1", branches=(1,), snr_db=(0.0, 15.0),
+                        cfo_hz=(-5000.0, 5000.0), win_start=PRE_PAD - 64, max_offset=128, seed=seed,
+                        device=device, dtype=dtype).x
 
 
 def make_aa_batch_torch(B: int, T: int = 1024, L: int = 512, *, seed: int = 2026, cir: str | None = "cir1",

@@ -459,6 +459,35 @@ def gen_post(R, cases):
     cases["post_streaming_peak"] = dict(kind="streaming_peak", metric=met, peak_bounded=np.int64(pk_b), **sp)
 
 
+def gen_synth(R, cases):
+    """Input builders the GPU synthesis restates (synth.py / synth.hip): the measured CIR banks
+    (channel.load_measured_cir, channel.py:15-48), the [A][A] preambles (sync_aa.build_aa_preamble,
+    sync_aa.py:160-235) and random QPSK OFDM symbols (sync_aa.build_random_qpsk_symbol,
+    sync_aa.py:238-260), plus one run_single_test frame chain without noise (convolution with the
+    CIR bank, sync_aa.py:577-634, and CFO, :637-645)."""
+    ch, sa = R["channel"], R["sync_aa"]
+    d = {}
+    for name in ("cir1", "cir2"):
+        d[name] = ch.load_measured_cir(name)
+    for ln in sa.PREAMBLE_LENGTHS:
+        d[f"pre{ln}"] = sa.build_aa_preamble(ln)[0]
+    rng = np.random.default_rng(7)
+    syms, qpsk = [], []
+    for _ in range(3):
+        s_, q_ = sa.build_random_qpsk_symbol(rng)
+        syms.append(s_)
+        qpsk.append(q_)
+    d["qpsk_symbols"], d["qpsk_values"] = np.array(syms), np.array(qpsk)
+    frame = np.concatenate([np.zeros(sa.TX_PRE_PAD_SAMPLES, complex), d["pre1024"], syms[0], syms[1],
+                            np.zeros(sa.TX_POST_PAD_SAMPLES, complex)])
+    cir = d["cir1"][:2]
+    rx = np.stack([np.convolve(frame, cir[a]) for a in range(2)])
+    d["frame_cir1_cfo500"] = sa.apply_cfo(rx, 500.0, sa.SAMPLE_RATE_HZ)
+    d["geometry"] = np.array([sa.N_FFT, sa.CYCLIC_PREFIX, sa.NUM_ACTIVE_SUBCARRIERS, sa.TX_PRE_PAD_SAMPLES,
+                              sa.TX_POST_PAD_SAMPLES])
+    cases["synth_builders"] = dict(kind="synth", **d)
+
+
 def main():
     R = _import_reference()
     cases: dict[str, dict] = {}
@@ -471,6 +500,7 @@ def main():
     gen_park(R, cases)
     gen_zc(R, cases)
     gen_post(R, cases)
+    gen_synth(R, cases)
     OUT.mkdir(parents=True, exist_ok=True)
     only = set(sys.argv[1:])               # optional case names: rewrite only those files
     for name, d in cases.items():

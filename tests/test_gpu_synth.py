@@ -78,3 +78,80 @@ def test_detector_recovers_drawn_cfo_and_offset():
     o0 = sync_aa.aa_detect_streaming_batched(x0, L=L)
     peak = o0.ev_int[:, 0, 0].cpu().numpy()
     assert np.max(np.abs(peak - (2 * L - 1))) <= 2
+
+
+# ---------------- ofs_synth_frames: the whole run_single_test chain per stream -----------------
+def _host_frame(fr, b, n_sym=2, fs=15.36e6):
+    """numpy restatement of sync_aa.run_single_test's chain for stream b without noise/ADC, from
+    the QPSK draws the GPU reports (synth.qpsk_symbol / frame pinned to the reference)."""
+    ph = fr.phases[b].cpu().numpy()
+    syms = [synth.qpsk_symbol(ph[s]) for s in range(n_sym)]
+    f = synth.frame(fr.preamble, syms)
+    rx = np.stack([np.convolve(f, fr.cir[br]) for br in range(fr.cir.shape[0])])
+    cfo = float(fr.params[b, 2])
+    return rx * np.exp(1j * 2 * np.pi * cfo * np.arange(rx.shape[1]) / fs)
+
+
+def test_frames_noiseless_equal_host_restatement():
+    B = 12
+    fr = synth.frames_batch(B, snr_db=(400.0, 400.0), seed=11, dtype=torch.complex128, return_phases=True)
+    x = fr.x.cpu().numpy()
+    assert x.shape == (B, 2, 500 + 1024 + 2 * 1096 + 500 + 1099)
+    for b in range(B):
+        ref = _host_frame(fr, b)
+        assert np.max(np.abs(x[b] - ref)) < 1e-11
+    ph = fr.phases.cpu().numpy()
+    assert ph.max() <= 3 and len(np.unique(ph[:, 0, :10], axis=0)) == B      # every stream its own payload
+
+
+def test_frames_noise_level_and_window():
+    B, fs = 64, 15.36e6
+    kw = dict(cir="cir2", seed=5, dtype=torch.complex128, cfo_hz=(700.0, 700.0))
+    clean = synth.frames_batch(B, snr_db=(400.0, 400.0), **kw)
+    noisy = synth.frames_batch(B, snr_db=(6.0, 6.0), **kw)
+    y, r = clean.x.cpu().numpy(), noisy.x.cpu().numpy()
+    Lout = y.shape[-1]
+    tone = np.exp(1j * 2 * np.pi * 700.0 * np.arange(Lout) / fs)
+    w = (r - y) * np.conj(tone)                                  # sd * g per branch
+    p_sig = np.mean(np.abs(y) ** 2, axis=-1)                     # mean |y_br|^2 (channel.py-style)
+    ratio = np.mean(np.abs(w) ** 2, axis=-1) / (p_sig / 10 ** 0.6)
+    assert abs(float(ratio.mean()) - 1.0) < 0.01 and float(ratio.std()) < 0.05
+    # a window: same samples, shifted by the drawn offset
+    win = synth.frames_batch(B, 1024, snr_db=(6.0, 6.0), win_start=300, max_offset=200, **kw)
+    st = win.params[:, 0].cpu().numpy().astype(int)
+    assert st.min() >= 300 and st.max() < 500 and len(set(st)) > 20
+    xw = win.x.cpu().numpy()
+    for b in range(B):
+        assert np.max(np.abs(xw[b] - r[b, :, st[b]:st[b] + 1024])) < 1e-12
+
+
+def test_frames_adc_codes():
+    B = 32
+    codes = synth.frames_batch(B, snr_db=(10.0, 10.0), full_scale_ratio=1.0, seed=9, dtype=torch.int16)
+    deq = synth.frames_batch(B, snr_db=(10.0, 10.0), full_scale_ratio=1.0, seed=9, dtype=torch.complex128)
+    c = codes.x.cpu().numpy().astype(np.float64)
+    assert c.min() >= -2048 and c.max() <= 2047
+    fsc = deq.params[:, 3].cpu().numpy()
+    d = deq.x.cpu().numpy()
+    assert np.array_equal(d.real, c[..., 0] / 2048 * fsc[:, None, None])       # quantize_adc's values
+    assert np.array_equal(d.imag, c[..., 1] / 2048 * fsc[:, None, None])
+    # full scale = rms over both branches: with ratio 1 about 16 % of the I/Q values clip
+    clipped = np.mean((c == -2048) | (c == 2047))
+    assert 0.05 < clipped < 0.35
+
+
+def test_frames_detected_like_run_single_test():
+    """2 antennas, cir1, 10 dB, 1024 preamble, 12-bit ADC at FS 1.0: the detector finds every frame,
+    timing within the reference's multipath range of the true start (sync_aa design doc: +77..+94
+    samples on multipath; grid golden cir1 +83)."""
+    B = 64
+    fr = synth.frames_batch(B, snr_db=(10.0, 10.0), full_scale_ratio=1.0, seed=21, dtype=torch.complex64)
+    out = sync_aa.aa_detect_streaming_batched(fr.x, L=512, outputs=())
+    n = out.n_events.cpu().numpy()
+    assert (n >= 1).all()
+    agg = np.sum(np.abs(fr.cir) ** 2, axis=0)
+    true_start = 500 + int(np.argmax(agg))                       # sync_aa.py:631-634, :718-719
+    fs_ = out.ev_int[:, 0, 3].cpu().numpy()
+    assert np.all(np.abs(fs_ - true_start) < 150)
+    cfo = out.ev_real[:, 0, 3].cpu().numpy()
+    assert np.all(np.abs(cfo - fr.params[:, 2].cpu().numpy()) < 300.0)

@@ -19,3 +19,46 @@ def test_zc_build_pss_symbol_leaves_zc_v2_globals_alone():
     finally:
         zc_v2.N_FFT, zc_v2.CYCLIC_PREFIX = n0, cp0
         zc.N_FFT, zc.CYCLIC_PREFIX = 2048, 512
+
+
+# ---- input builders of the synthesis, pinned to the reference's own outputs -----------------
+import os  # noqa: E402
+
+from conftest import GOLDEN  # noqa: E402
+from ofdm_sync_amd import synth  # noqa: E402
+
+
+def _syn():
+    return np.load(os.path.join(GOLDEN, "synth_builders.npz"), allow_pickle=False)
+
+
+def test_load_cir_matches_reference():
+    d = _syn()
+    for name in ("cir1", "cir2"):
+        assert np.array_equal(synth.load_cir(name), d[name])          # channel.load_measured_cir
+
+
+def test_aa_preamble_matches_reference():
+    d = _syn()
+    for ln in (1024, 512, 256):
+        np.testing.assert_allclose(synth.aa_preamble(ln), d[f"pre{ln}"], rtol=0, atol=1e-12)
+    g = np.load(os.path.join(GOLDEN, "aa_clean_L512.npz"))
+    np.testing.assert_allclose(synth.aa_preamble(1024), g["x"][0, 500:1524], rtol=0, atol=1e-12)
+
+
+def test_qpsk_symbol_and_frame_chain_match_reference():
+    d = _syn()
+    N, cp, K, pre, post = (int(v) for v in d["geometry"])
+    assert (N, cp, K, pre, post) == (synth.N_FFT, synth.CYCLIC_PREFIX, synth.NUM_ACTIVE, synth.PRE_PAD, synth.POST_PAD)
+    syms = []
+    for q, ref in zip(d["qpsk_values"], d["qpsk_symbols"]):
+        ph = np.mod(np.round((np.angle(q * np.sqrt(2)) / (np.pi / 4) - 1) / 2), 4).astype(int)
+        s = synth.qpsk_symbol(ph)
+        np.testing.assert_allclose(s, ref, rtol=0, atol=1e-12)
+        syms.append(s)
+    fr = synth.frame(synth.aa_preamble(1024), syms[:2])
+    cir = synth.load_cir("cir1")[:2]
+    rx = np.stack([np.convolve(fr, cir[a]) for a in range(2)])
+    n = np.arange(rx.shape[1])
+    rx = rx * np.exp(1j * 2 * np.pi * 500.0 * n / 15.36e6)
+    np.testing.assert_allclose(rx, d["frame_cir1_cfo500"], rtol=0, atol=1e-12)
