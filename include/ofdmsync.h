@@ -32,6 +32,13 @@ extern "C" {
 #define OFS_C64   0   /* interleaved float32 (re, im)                                  */
 #define OFS_C128  1   /* interleaved float64 (re, im)                                  */
 #define OFS_CI16  2   /* interleaved int16 (I, Q), e.g. 12-bit ADC words sign-extended  */
+/* packed 12-bit AXIS words, the RTL detector's wire format (ref/test_minn_preamble_detector.py:41-47,
+ * ref/minn_preamble_detector.sv:152-155): per time index one word of n_ant 24-bit channel groups,
+ * channel c at bit 24*c with I in its bits 0-11 and Q in 12-23 (two's complement), words packed
+ * back to back little-endian (3 * n_ant bytes per time index); layout [B][T][3 * n_ant] bytes.
+ * Accepted by ofs_aa_detect (OFS_FP64, 1-2 antennas) and ofs_minn_rtl (1-2 branches) on their
+ * integer-exact plans; other entry points / shapes return OFS_EINVAL. */
+#define OFS_CP12  3
 
 /* arithmetic precision of a call */
 #define OFS_FP32  0   /* fp32 products / in-row scans, fp64 row bases; f32/c64 outputs  */

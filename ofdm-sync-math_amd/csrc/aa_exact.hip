@@ -51,6 +51,55 @@ __device__ __forceinline__ void load_words(const int32_t* xs, int64_t n0, int64_
         for (int e = 0; e < E; ++e) w[e] = (n0 + e < T) ? xs[n0 + e] : 0;
     }
 }
+// OFS_CP12: E consecutive time indices n0.. of the NA channels of one stream (base x8), decoded
+// to the int16 I/Q words above.  Fast path: the lane's 3·NA·E bytes with dword loads from the
+// dword below, realigned with v_alignbyte (groups then sit at compile-time byte offsets); used
+// when the row is whole and the rounded-up dword window stays inside the buffer.  Otherwise per
+// byte with zero fill past T.
+__device__ __forceinline__ int32_t cp12_word(uint32_t g) {
+    const int32_t i = ((int32_t)(g << 20)) >> 20;              // bits 0-11, sign-extended
+    const int32_t q = ((int32_t)(g << 8)) >> 20;               // bits 12-23
+    return (i & 0xffff) | (int32_t)((uint32_t)q << 16);
+}
+template <int E, int NA>
+__device__ __forceinline__ void cp12_load(const uint8_t* x8, int64_t sbyte, int64_t n0, int64_t T, int64_t total,
+                                          int32_t (&w)[NA][E]) {
+    constexpr int NB = 3 * NA * E;                              // bytes wanted
+    constexpr int ND = (NB + 3 + 3) / 4;                        // dwords covering them at any shift
+    const int64_t p = sbyte + 3 * NA * n0;                      // absolute byte offset in the buffer
+    const int64_t a = p & ~(int64_t)3;
+    if (n0 + E <= T && a + 4 * ND <= total) {
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(x8 - sbyte + a);
+        uint32_t v[ND];
+#pragma unroll
+        for (int j = 0; j < ND; ++j) v[j] = d[j];
+        const uint32_t sh = (uint32_t)(p & 3);
+        uint32_t al[ND - 1];                                    // bytes p, p+1, ... in order
+#pragma unroll
+        for (int j = 0; j + 1 < ND; ++j) al[j] = __builtin_amdgcn_alignbyte(v[j + 1], v[j], sh);
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+            for (int t = 0; t < NA; ++t) {
+                const int bo = 3 * (e * NA + t);                // compile-time after unrolling
+                const uint64_t win = ((uint64_t)al[bo / 4 + 1 < ND - 1 ? bo / 4 + 1 : ND - 2] << 32) | al[bo / 4];
+                w[t][e] = cp12_word((uint32_t)(win >> (8 * (bo & 3))) & 0xffffffu);
+            }
+    } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+            for (int t = 0; t < NA; ++t) {
+                if (n0 + e < T) {
+                    const uint8_t* q = x8 + 3 * (NA * (n0 + e) + t);
+                    w[t][e] = cp12_word((uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16));
+                } else {
+                    w[t][e] = 0;
+                }
+            }
+    }
+}
+
 __device__ __forceinline__ double w_re(int32_t w) { return (double)(int16_t)(w & 0xffff); }
 __device__ __forceinline__ double w_im(int32_t w) { return (double)(w >> 16); }
 
@@ -101,7 +150,7 @@ struct RowPrefix {
 // ------------------------------------------------------------------------------------------
 template <int FMT, int E, int MR, int NA>
 __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1) void aa_exact_kernel(AaFastArgs a) {
-    using X = XSamp<FMT>;
+    using X = XSamp<FMT == OFS_CP12 ? OFS_CI16 : FMT>;          // CP12 decodes to int16 I/Q words
     using W = typename X::W;
     constexpr int RL = 64 * E;
     constexpr int L = MR * RL;
@@ -113,6 +162,17 @@ __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1
     const int64_t T = a.T;
     const int nrows = (int)((T + RL - 1) / RL);
     const W* xs = reinterpret_cast<const W*>(a.x) + b * NA * T;
+    const int64_t sbyte = b * NA * T * 3;                        // CP12: stream start in bytes
+    const uint8_t* x8 = reinterpret_cast<const uint8_t*>(a.x) + sbyte;
+    const int64_t total = a.B * NA * T * 3;
+    auto load_all = [&](int64_t n0, W (&dst)[NA][E]) {
+        if constexpr (FMT == OFS_CP12) {
+            cp12_load<E, NA>(x8, sbyte, n0, T, total, dst);
+        } else {
+#pragma unroll
+            for (int t = 0; t < NA; ++t) X::template load<E>(xs + t * T, n0, T, dst[t]);
+        }
+    };
 
     W lag[NA][MR][E];                                        // raw samples of rows k-MR..k-1
     double Ar[MR][E], Ai[MR][E], Ae[MR][E];                  // prefix values of rows k-MR..k-1
@@ -128,9 +188,7 @@ __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1
 
     W nx[PD][NA][E];
 #pragma unroll
-    for (int p = 0; p < PD; ++p)
-#pragma unroll
-        for (int t = 0; t < NA; ++t) X::template load<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
+    for (int p = 0; p < PD; ++p) load_all((int64_t)RL * p + E * lane, nx[p]);
 
     AaRowGate<E, double, false, true, FMT != OFS_C128> gate;
     if (a.detect)
@@ -153,11 +211,7 @@ __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1
                 for (int t = 0; t < NA; ++t)
 #pragma unroll
                     for (int e = 0; e < E; ++e) cur[t][e] = nx[u % PD][t][e];
-                if (k + PD < nrows) {
-#pragma unroll
-                    for (int t = 0; t < NA; ++t)
-                        X::template load<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[u % PD][t]);
-                }
+                if (k + PD < nrows) load_all((int64_t)RL * (k + PD) + E * lane, nx[u % PD]);
                 const int sl = u % MR;                       // ring slot of row k-MR (and k)
                 double pr[E], pi[E], en[E];
 #pragma unroll
@@ -281,7 +335,7 @@ __device__ __forceinline__ bool same_bits(double a, double b) {
     return __double_as_longlong(a) == __double_as_longlong(b);
 }
 
-template <int E, int MW>
+template <int E, int MW, int CPNA>
 __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #pragma clang fp contract(off)
     constexpr int RL = 64 * E;
@@ -306,6 +360,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     auto hx = [&](int t, int m, int e) -> int32_t& { return hx_[((t * MW + m) * E + e) * 64 + lane]; };
     const int nrows = (int)((T + RL - 1) / RL);
     const int32_t* xs = reinterpret_cast<const int32_t*>(a.x) + b * nb_ * T;
+    const int64_t sbyte = b * nb_ * T * 3;                         // CP12 (CPNA branches)
+    const uint8_t* x8 = reinterpret_cast<const uint8_t*>(a.x) + sbyte;
+    const int64_t total = a.B * nb_ * T * 3;
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -335,15 +392,27 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     constexpr int PD = E == 1 ? 8 : (E == 2 ? 4 : 2);
     constexpr int NBM = 4;                                         // branches supported
     int32_t nx[PD][NBM][E];
+    // one row of every branch (CPNA > 0: packed 12-bit words, CPNA branches)
+    auto load_row = [&](int64_t n0, int32_t (&dst)[NBM][E]) {
+        if constexpr (CPNA > 0) {
+            int32_t w[CPNA][E];
+            cp12_load<E, CPNA>(x8, sbyte, n0, T, total, w);
 #pragma unroll
-    for (int p = 0; p < PD; ++p)
+            for (int t = 0; t < NBM; ++t)
 #pragma unroll
-        for (int t = 0; t < NBM; ++t) {
-            if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * p + E * lane, T, nx[p][t]);
-            else
+                for (int e = 0; e < E; ++e) dst[t][e] = t < CPNA ? w[t < CPNA ? t : 0][e] : 0;
+        } else {
 #pragma unroll
-                for (int e = 0; e < E; ++e) nx[p][t][e] = 0;
+            for (int t = 0; t < NBM; ++t) {
+                if (t < nb_) load_words<E>(xs + t * T, n0, T, dst[t]);
+                else
+#pragma unroll
+                    for (int e = 0; e < E; ++e) dst[t][e] = 0;
+            }
         }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load_row((int64_t)RL * p + E * lane, nx[p]);
 
     const int nseg = (int)((T + SEG - 1) / SEG);
     for (int g = 0; g < nseg; ++g) {
@@ -364,11 +433,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 for (int t = 0; t < NBM; ++t)
 #pragma unroll
                     for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
-            if (k + PD < nrows) {
-#pragma unroll
-                for (int t = 0; t < NBM; ++t)
-                    if (t < nb_) load_words<E>(xs + t * T, (int64_t)RL * (k + PD) + E * lane, T, nx[PD - 1][t]);
-            }
+            if (k + PD < nrows) load_row((int64_t)RL * (k + PD) + E * lane, nx[PD - 1]);
             double pc[E], en[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
@@ -567,6 +632,8 @@ template <int E, int MR, int NA>
 int aa_launch(int fmt, const AaFastArgs& a, hipStream_t st) {
     if (fmt == OFS_C128)
         hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+    else if (fmt == OFS_CP12)
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CP12, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
     else
         hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
@@ -590,15 +657,15 @@ int aa_launch_mr(int fmt, int mr, int na, const AaFastArgs& a, hipStream_t st) {
     return 0;
 }
 
-template <int E, int MW>
-int rtl_launch(const RtlExactArgs& a, hipStream_t st) {
+template <int E, int MW, int CPNA>
+int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
     const size_t per_wave = rtl_wave_lds(E, MW, a.nb);
     int wpb = 4;                                             // waves (streams) per workgroup
     const char* ev = getenv("OFS_RTL_WPB");                  // tuning: 1, 2 or 4
     if (ev && (atoi(ev) == 1 || atoi(ev) == 2)) wpb = atoi(ev);
     while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
     const size_t lds = per_wave * wpb;
-    auto k = rtl_exact_kernel<E, MW>;
+    auto k = rtl_exact_kernel<E, MW, CPNA>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return OFS_EHIP;
@@ -606,14 +673,22 @@ int rtl_launch(const RtlExactArgs& a, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
+template <int E, int MW>
+int rtl_launch(int fmt, const RtlExactArgs& a, hipStream_t st) {
+    if (fmt == OFS_CP12) return a.nb == 1 ? rtl_launch_k<E, MW, 1>(a, st) : rtl_launch_k<E, MW, 2>(a, st);
+    return rtl_launch_k<E, MW, 0>(a, st);
+}
+
 }  // namespace
 
 // 10*E + MR of the wave-per-stream fp64 aa kernel for a shape (+100 for complex128 input), 0 if
 // not covered
 int ofs_aa_exact_plan(int fmt, int precision, int n_ant, int64_t T, int L) {
-    if ((fmt != OFS_CI16 && fmt != OFS_C128) || precision != OFS_FP64 || n_ant < 1 || n_ant > 2 || !exact_enabled())
+    if ((fmt != OFS_CI16 && fmt != OFS_C128 && fmt != OFS_CP12) || precision != OFS_FP64 || n_ant < 1 || n_ant > 2 ||
+        (!exact_enabled() && fmt != OFS_CP12))
         return 0;
-    if (fmt == OFS_CI16 && (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2)) return 0;   // sums < 2^53
+    if ((fmt == OFS_CI16 || fmt == OFS_CP12) && (T < 1 || T * n_ant > (1 << 21) || T > 0x7fffffff / 2))
+        return 0;                                                // sums < 2^53
     // complex128: stream-wide fp64 prefix differences.  Their error, O(eps·|prefix|) <=
     // O(eps·n·max term), is of the same order as the reference's own recursive running sum
     // (sum = sum + new - oldest, sync_aa.py:331-342, which accumulates O(eps·n·max term)), so
@@ -636,7 +711,8 @@ int ofs_aa_exact_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hip
 }
 
 int ofs_rtl_exact_plan(int fmt, int n_br, int64_t T, int Q) {
-    if (fmt != OFS_CI16 || n_br < 1 || n_br > 4 || !exact_enabled()) return 0;
+    if (fmt == OFS_CP12 ? (n_br < 1 || n_br > 2) : (fmt != OFS_CI16 || n_br < 1 || n_br > 4 || !exact_enabled()))
+        return 0;
     if (T < 1 || T * n_br > (1 << 21)) return 0;
     for (int e : {1, 2, 4}) {
         if (Q % (64 * e)) continue;
@@ -658,12 +734,12 @@ int ofs_rtl_exact_try(int fmt, int n_br, const RtlExactCall& c, hipStream_t st) 
     a.max_ev = c.max_ev; a.n_ev = c.n_ev; a.ev = c.ev; a.open_start = c.open_start;
 
     switch (plan) {
-        case 11: return rtl_launch<1, 1>(a, st);
-        case 12: return rtl_launch<1, 2>(a, st);
-        case 21: return rtl_launch<2, 1>(a, st);
-        case 22: return rtl_launch<2, 2>(a, st);
-        case 41: return rtl_launch<4, 1>(a, st);
-        case 42: return rtl_launch<4, 2>(a, st);
+        case 11: return rtl_launch<1, 1>(fmt, a, st);
+        case 12: return rtl_launch<1, 2>(fmt, a, st);
+        case 21: return rtl_launch<2, 1>(fmt, a, st);
+        case 22: return rtl_launch<2, 2>(fmt, a, st);
+        case 41: return rtl_launch<4, 1>(fmt, a, st);
+        case 42: return rtl_launch<4, 2>(fmt, a, st);
     }
     return 0;
 }

@@ -836,7 +836,8 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
                       int32_t detect, double threshold, int32_t hysteresis, double sample_rate,
                       int32_t max_events, int32_t* n_events, int64_t* ev_int, double* ev_real,
                       void* stream) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_ant < 1 || T < 0 || L < 1)
+    if (!(fmt_ok(in_fmt) || in_fmt == OFS_CP12) || !prec_ok(precision) || OFS_MISSING(x, B * T) || B < 0 || n_ant < 1 ||
+        T < 0 || L < 1)
         return OFS_EINVAL;
     if (detect && (OFS_MISSING(n_events, B) || max_events < 0 ||
                    (max_events > 0 && B > 0 && (!ev_int || !ev_real))))
@@ -855,6 +856,7 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
         if (frc == 1) return OFS_OK;
         if (frc < 0) return frc;
     }
+    if (in_fmt == OFS_CP12) return OFS_EINVAL;                        // packed words: exact kernels only
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = T; a.nb = n_ant; a.D = L; a.W = L;
     a.P = P; a.R = R; a.M = M; a.valid = valid;
@@ -887,11 +889,12 @@ int32_t ofs_aa_detect(int32_t in_fmt, const void* x, int64_t B, int32_t n_ant, i
 }
 
 int32_t ofs_aa_plan(int32_t in_fmt, int32_t precision, int32_t n_ant, int64_t T, int32_t L) {
-    if (!fmt_ok(in_fmt) || !prec_ok(precision) || n_ant < 1 || T < 0 || L < 1) return OFS_EINVAL;
+    if (!(fmt_ok(in_fmt) || in_fmt == OFS_CP12) || !prec_ok(precision) || n_ant < 1 || T < 0 || L < 1) return OFS_EINVAL;
     const int fp = ofs_aa_fast_plan(in_fmt, precision, n_ant, T, L);
     if (fp) return 1000 + fp;
     const int xp = ofs_aa_exact_plan(in_fmt, precision, n_ant, T, L);
     if (xp) return (xp >= 100 ? 3000 : 2000) + xp % 100;
+    if (in_fmt == OFS_CP12) return OFS_EINVAL;
     if (2 * (int64_t)L - 1 > 0x3fffffff) return OFS_ETOOLONG;
     Plan p;
     const int lo = -(int)(2 * (int64_t)L - 1);
@@ -949,7 +952,8 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
                      int32_t detect, int32_t hysteresis, int32_t timing_offset,
                      int32_t max_events, int32_t* n_events, int64_t* events,
                      int64_t* open_gate_start, void* stream) {
-    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0 || Q < 1) return OFS_EINVAL;
+    if (!(fmt_ok(in_fmt) || in_fmt == OFS_CP12) || OFS_MISSING(x, B * T) || B < 0 || n_br < 1 || T < 0 || Q < 1)
+        return OFS_EINVAL;
     if (OFS_MISSING(corr_total, B * T) || OFS_MISSING(energy_total, B * T) || smooth_shift < 0 || smooth_shift > 62 ||
         threshold_frac_bits < 0 || threshold_frac_bits > 62 || (smooth_mode != 0 && smooth_mode != 1))
         return OFS_EINVAL;
@@ -971,6 +975,7 @@ int32_t ofs_minn_rtl(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int
         if (frc == 1) return OFS_OK;
         if (frc < 0) return frc;
     }
+    if (in_fmt == OFS_CP12) return OFS_EINVAL;                        // packed words: exact kernel only
     WinArgs a{};
     a.x = x; a.T = T; a.n_out = T; a.nb = n_br; a.Q = Q; a.D = Q; a.W = Q;
     a.corr_total = corr_total; a.corr_positive = corr_positive; a.energy_total = energy_total;

@@ -17,7 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("OFS_LIB") or os.path.join(_HERE, "libofdmsync.so")   # OFS_LIB: tuning builds
 
 # input formats / precisions / status (include/ofdmsync.h)
-C64, C128, CI16 = 0, 1, 2
+C64, C128, CI16, CP12 = 0, 1, 2, 3
 FP32, FP64 = 0, 1
 
 _lib = None
@@ -178,7 +178,9 @@ def as_batch(x, batched: bool, *, complex_cast: bool = False) -> Batch:
     from_numpy = not isinstance(x, torch.Tensor)
     if from_numpy:
         a = np.asarray(x)
-        if a.dtype == np.int16 and a.ndim >= 1 and a.shape[-1] == 2:
+        if a.dtype == np.uint8 and a.ndim >= 2 and a.shape[-1] % 3 == 0:
+            t = torch.from_numpy(np.ascontiguousarray(a))
+        elif a.dtype == np.int16 and a.ndim >= 1 and a.shape[-1] == 2:
             t = torch.from_numpy(np.ascontiguousarray(a))
         else:
             if complex_cast or not np.iscomplexobj(a) or a.dtype not in (np.complex64, np.complex128):
@@ -189,10 +191,24 @@ def as_batch(x, batched: bool, *, complex_cast: bool = False) -> Batch:
         t = x
         if t.device.type != "cuda":
             t = t.to(dev)
-        if complex_cast and t.dtype != torch.complex128 and t.dtype != torch.int16:
+        packed = t.dtype == torch.uint8 and t.dim() >= 2 and t.shape[-1] % 3 == 0
+        if complex_cast and t.dtype != torch.complex128 and t.dtype != torch.int16 and not packed:
             t = t.to(torch.complex128)
-        if not (t.is_complex() or (t.dtype == torch.int16 and t.shape[-1] == 2)):
+        if not (t.is_complex() or (t.dtype == torch.int16 and t.shape[-1] == 2) or packed):
             t = t.to(torch.complex128)
+    if t.dtype == torch.uint8:
+        # packed 12-bit AXIS words [.., T, 3 * n_ch] (OFS_CP12): channels live in the last axis
+        fmt = CP12
+        n_ch = t.shape[-1] // 3
+        lead = tuple(t.shape[:-2])
+        Tn = t.shape[-2]
+        if batched:
+            if len(lead) != 1:
+                raise ValueError("batched packed input must be [B, T, 3 * n_ch] uint8")
+            return Batch(t.contiguous(), fmt, lead[0], n_ch, Tn, from_numpy, True)
+        if len(lead) != 0:
+            raise ValueError("packed input must be [T, 3 * n_ch] uint8")
+        return Batch(t.contiguous(), fmt, 1, n_ch, Tn, from_numpy, True)
     if t.dtype == torch.int16:
         fmt = CI16
         core_shape = tuple(t.shape[:-1])

@@ -62,3 +62,31 @@ def test_qpsk_symbol_and_frame_chain_match_reference():
     n = np.arange(rx.shape[1])
     rx = rx * np.exp(1j * 2 * np.pi * 500.0 * n / 15.36e6)
     np.testing.assert_allclose(rx, d["frame_cir1_cfo500"], rtol=0, atol=1e-12)
+
+
+# ---- wire formats (OFS_CP12 packing, the reference's .hex test vector) ----------------------
+from ofdm_sync_amd import wire  # noqa: E402
+
+
+def test_axis_pack_matches_reference_packing():
+    """Bit layout of ref/test_minn_preamble_detector.py:41-47 (_pack_axis_samples), restated:
+    word = ch0_i | ch0_q << 12 | ch1_i << 24 | ch1_q << 36 (12-bit two's complement fields)."""
+    rng = np.random.default_rng(1)
+    iq = rng.integers(-2048, 2048, size=(3, 2, 17, 2)).astype(np.int16)    # [B, ch, T, IQ]
+    w = wire.pack_axis(iq)
+    assert w.shape == (3, 17, 6) and w.dtype == np.uint8
+    m = (1 << 12) - 1
+    for b in range(3):
+        for n in range(17):
+            word = ((int(iq[b, 0, n, 0]) & m) | ((int(iq[b, 0, n, 1]) & m) << 12) |
+                    ((int(iq[b, 1, n, 0]) & m) << 24) | ((int(iq[b, 1, n, 1]) & m) << 36))
+            assert int.from_bytes(bytes(w[b, n]), "little") == word
+    assert np.array_equal(wire.unpack_axis(w), iq)
+
+
+def test_hex_vector_is_the_preamble():
+    """docs/preamble_test_vector.hex = (re12 << 12) | im12 of round(preamble * 1024)."""
+    iq = wire.read_hex_vector(os.path.join(GOLDEN, "preamble_test_vector.hex"))
+    pre = synth.aa_preamble(1024)
+    assert iq.shape == (1024, 2)
+    assert np.array_equal(iq[:, 0], np.round(pre.real * 1024)) and np.array_equal(iq[:, 1], np.round(pre.imag * 1024))

@@ -95,10 +95,18 @@ def int12(x):
     return torch.stack([re, im], dim=-1).contiguous()
 
 
-def cfg2a(dev, st, steps, warmup):
-    """cfg2 (aa side): sync_aa detector, L=128, int12 I/Q, B=4096 x T=1024, fp64 (bit-exact)."""
+def packed(x):
+    """int16 I/Q [B, n_ch, T, 2] (device) -> packed 12-bit AXIS words [B, T, 3 n_ch] (OFS_CP12)."""
+    from ofdm_sync_amd import wire
+    return torch.from_numpy(wire.pack_axis(x.cpu().numpy())).to(x.device)
+
+
+def cfg2a(dev, st, steps, warmup, cp12=False):
+    """cfg2 (aa side): sync_aa detector, L=128, int12 I/Q, B=4096 x T=1024, fp64 (bit-exact);
+    cp12: the same samples as packed 12-bit AXIS words (3 B/sample instead of 4)."""
     B, T, L = 4096, 1024, 128
-    x = dput(dev, int12(synth.make_aa_batch(B, T, L, seed=7, device=dev)))
+    x = int12(synth.make_aa_batch(B, T, L, seed=7, device=dev))
+    x = dput(dev, packed(x) if cp12 else x)
     P = dbuf(dev, (B, T), torch.complex128)
     R = dbuf(dev, (B, T), torch.float64)
     M = dbuf(dev, (B, T), torch.float64)
@@ -108,23 +116,29 @@ def cfg2a(dev, st, steps, warmup):
     ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
     ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
     L_ = _lib.lib()
-    args = (_lib.CI16, x.data_ptr(), B, 1, T, L, _lib.FP64, P.data_ptr(), R.data_ptr(), M.data_ptr(),
+    fmt = _lib.CP12 if cp12 else _lib.CI16
+    args = (fmt, x.data_ptr(), B, 1, T, L, _lib.FP64, P.data_ptr(), R.data_ptr(), M.data_ptr(),
             V.data_ptr(), 1, 0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(),
             st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa"), steps, warmup, st)
-    nbytes = B * T * (4 + 16 + 8 + 8 + 1)
-    plan = L_.ofs_aa_plan(_lib.CI16, _lib.FP64, 1, T, L)
+    insz = 3 if cp12 else 4
+    nbytes = B * T * (insz + 16 + 8 + 8 + 1)
+    plan = L_.ofs_aa_plan(fmt, _lib.FP64, 1, T, L)
     kernel = (f"aa_exact_kernel<E={(plan - 2000) // 10},MR={plan % 10}> (integer-exact, wave per stream, "
               "fused events)" if plan > 2000 else "win_kernel<CI16,fp64,AA> (fused events)")
-    return dict(config="cfg2a", workload=f"sync_aa detector L={L}, int12 I/Q, {B} x {T}, fp64",
+    return dict(config="cfg2a_cp12" if cp12 else "cfg2a",
+                workload=f"sync_aa detector L={L}, int12 {'packed AXIS words' if cp12 else 'I/Q'}, {B} x {T}, fp64",
                 kernel=kernel, samples=B * T, ms=ms, alg_bytes=nbytes,
-                bytes_per_sample="4 in + P 16 + R 8 + M 8 + valid 1")
+                bytes_per_sample=f"{insz} in + P 16 + R 8 + M 8 + valid 1")
 
 
-def cfg2b(dev, st, steps, warmup):
-    """cfg2 (minn_rtl side): Q=64, int12 I/Q, B=4096 x T=1024, fused IIR + threshold + gate."""
+def cfg2b(dev, st, steps, warmup, cp12=False):
+    """cfg2 (minn_rtl side): Q=64, int12 I/Q, B=4096 x T=1024, fused IIR + threshold + gate;
+    cp12: packed 12-bit AXIS words."""
     B, T, Q = 4096, 1024, 64
     x = int12(synth.make_aa_batch(B, T, 128, seed=9, device=dev))
+    if cp12:
+        x = packed(x)
     f = lambda: torch.empty((B, T), dtype=torch.float64, device=dev)   # noqa: E731
     b = lambda: torch.empty((B, T), dtype=torch.bool, device=dev)      # noqa: E731
     o = [f(), f(), f(), f(), f(), f(), b(), b()]
@@ -138,16 +152,20 @@ def cfg2b(dev, st, steps, warmup):
     if parts == "metric":
         ptrs = [ptrs[0], ptrs[1], None, ptrs[3], None, ptrs[5], ptrs[6], None]
     det = 0 if parts in ("metric", "smooth") else 1
-    args = (_lib.CI16, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *ptrs, det, 2, 0, E,
+    fmt = _lib.CP12 if cp12 else _lib.CI16
+    args = (fmt, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *ptrs, det, 2, 0, E,
             n_ev.data_ptr(), ev.data_ptr(), og.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_minn_rtl(*args), "minn_rtl"), steps, warmup, st)
-    nbytes = B * T * (4 + 6 * 8 + 2)
-    plan = L_.ofs_rtl_plan(_lib.CI16, 1, T, Q)
+    insz = 3 if cp12 else 4
+    nbytes = B * T * (insz + 6 * 8 + 2)
+    plan = L_.ofs_rtl_plan(fmt, 1, T, Q)
     kernel = (f"rtl_exact_kernel<E={(plan - 2000) // 10},MW={plan % 10}> (integer-exact metric + in-wave "
               "IIR + closed-form gate)" if plan else "win_kernel<CI16,fp64,RTL> + rtl_iir_kernel")
-    return dict(config="cfg2b", workload=f"minn_rtl Q={Q}, int12 I/Q, {B} x {T}, fp64 + sequential IIR/gate",
+    return dict(config="cfg2b_cp12" if cp12 else "cfg2b",
+                workload=f"minn_rtl Q={Q}, int12 {'packed AXIS words' if cp12 else 'I/Q'}, {B} x {T}, fp64 + "
+                         "sequential IIR/gate",
                 kernel=kernel, samples=B * T, ms=ms, alg_bytes=nbytes,
-                bytes_per_sample="4 in + 6 x f64 8 + 2 flags")
+                bytes_per_sample=f"{insz} in + 6 x f64 8 + 2 flags")
 
 
 def cfg4(dev, st, steps, warmup, B=32768, seed=4):
@@ -414,7 +432,8 @@ def aa_refshape_c128(dev, st, steps, warmup):
                    "sync_aa S&C fp64 L=512, 16384 x 2 ant x 5315 c128 (reference run_single_test shape)", 43)
 
 
-CONFIGS = {"cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
+CONFIGS = {"cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
+           "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 

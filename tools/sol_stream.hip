@@ -95,6 +95,46 @@ __global__ __launch_bounds__(256) void pattern_lds(const float4* __restrict__ x,
     }
 }
 
+// the cfg4 pattern (fused combined S&C + Minn, combined_sc_min.py:333-335): 8 B read and two
+// output sets of P c64 + R f32 + M f32 = 32 B written per sample (1:4), flat, 16 B per lane
+__global__ void pattern_cfg4(const float4* __restrict__ x, float4* __restrict__ P1, float4* __restrict__ R1,
+                             float4* __restrict__ M1, float4* __restrict__ P2, float4* __restrict__ R2,
+                             float4* __restrict__ M2, int64_t nq) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = x[2 * q], c = x[2 * q + 1];
+        const float4 r = make_float4(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w, c.x * c.x + c.y * c.y,
+                                     c.z * c.z + c.w * c.w);
+        P1[2 * q] = a; P1[2 * q + 1] = c; R1[q] = r; M1[q] = make_float4(r.x * 0.5f, r.y, r.z, r.w);
+        P2[2 * q] = c; P2[2 * q + 1] = a; R2[q] = make_float4(r.w, r.z, r.y, r.x);
+        M2[q] = make_float4(r.x * 0.25f, r.y, r.z, r.w);
+    }
+}
+
+// the same 1:4 mix with 8 B per lane (float2) stores at a 4-byte-misaligned base, as the fused
+// kernel's [B][T-N+1] output rows force (odd row length, d0 = nb - (N-1))
+__global__ void pattern_cfg4_f2(const float4* __restrict__ x, float2* __restrict__ P1, float2* __restrict__ R1,
+                                float2* __restrict__ M1, float2* __restrict__ P2, float2* __restrict__ R2,
+                                float2* __restrict__ M2, int64_t nh) {
+    for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < nh; h += (int64_t)gridDim.x * blockDim.x) {
+        const float4 a = x[h];
+        const float2 r = make_float2(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w);
+        float* p1 = reinterpret_cast<float*>(P1) + 1;             // misaligned by one float
+        float* r1 = reinterpret_cast<float*>(R1) + 1;
+        float* m1 = reinterpret_cast<float*>(M1) + 1;
+        float* p2 = reinterpret_cast<float*>(P2) + 1;
+        float* r2 = reinterpret_cast<float*>(R2) + 1;
+        float* m2 = reinterpret_cast<float*>(M2) + 1;
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+        typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
+        *reinterpret_cast<f4u*>(p1 + 4 * h) = f4u{a.x, a.y, a.z, a.w};
+        *reinterpret_cast<f2u*>(r1 + 2 * h) = f2u{r.x, r.y};
+        *reinterpret_cast<f2u*>(m1 + 2 * h) = f2u{r.x * 0.5f, r.y};
+        *reinterpret_cast<f4u*>(p2 + 4 * h) = f4u{a.z, a.w, a.x, a.y};
+        *reinterpret_cast<f2u*>(r2 + 2 * h) = f2u{r.y, r.x};
+        *reinterpret_cast<f2u*>(m2 + 2 * h) = f2u{r.x * 0.25f, r.y};
+    }
+}
+
 // read-only and write-only streams
 __global__ void read4(const float4* __restrict__ a, float* out, int64_t n4) {
     float s = 0.f;
@@ -170,6 +210,20 @@ int main(int argc, char** argv) {
            time_ms([&] { pattern_lds<1024, 256><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
     report("pattern_lds<NV=512>", 24.0 * n,
            time_ms([&] { pattern_lds<1024, 512><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    {   // cfg4 mix: 8 B in, 32 B out per sample (same sample count)
+        float4 *P2, *R2, *M2;
+        CK(hipMalloc(&P2, n * 8 + 64)); CK(hipMalloc(&R2, n * 4 + 64)); CK(hipMalloc(&M2, n * 4 + 64));
+        float4 *P1b, *R1b, *M1b;
+        CK(hipMalloc(&P1b, n * 8 + 64)); CK(hipMalloc(&R1b, n * 4 + 64)); CK(hipMalloc(&M1b, n * 4 + 64));
+        for (int grid_mult : {8, 16}) {
+            snprintf(nm, sizeof nm, "pattern_cfg4(8r+32w, 16B stores) grid=%dxCU", grid_mult);
+            report(nm, 40.0 * n, time_ms([&] { pattern_cfg4<<<cus * grid_mult, 256>>>(x, P1b, R1b, M1b, P2, R2, M2, n / 4); }, iters));
+            snprintf(nm, sizeof nm, "pattern_cfg4_f2(8r+32w, misaligned 8B stores) grid=%dxCU", grid_mult);
+            report(nm, 40.0 * n, time_ms([&] { pattern_cfg4_f2<<<cus * grid_mult, 256>>>(x, (float2*)P1b, (float2*)R1b, (float2*)M1b,
+                                                                                         (float2*)P2, (float2*)R2, (float2*)M2, n / 2); }, iters));
+        }
+        CK(hipFree(P2)); CK(hipFree(R2)); CK(hipFree(M2)); CK(hipFree(P1b)); CK(hipFree(R1b)); CK(hipFree(M1b));
+    }
     report("pattern_wave(8r+16w) wave-per-stream again", 24.0 * n,
            time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
     return 0;
