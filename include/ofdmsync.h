@@ -325,6 +325,12 @@ int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N
  */
 int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                void** plan, size_t* work_bytes);
+/* As ofs_zc_fft_plan_create; prune_bins > 0 (N a power of two <= 4096) makes the plan PRUNED: a
+ * rocFFT store callback keeps only the template bins, so ofs_zc_freq_metric_fft's `spectrum` is
+ * a compact [n_windows][prune_bins] buffer (n_bins must equal prune_bins) and the dense N-point
+ * spectrum never reaches HBM.  prune_bins == 0: the dense plan. */
+int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, void** plan_out, size_t* work_bytes);
 int32_t ofs_zc_fft_plan_destroy(void* plan);
 /*
  * For each offset off in [0, T-(N+cp)]: one batched rocFFT of x[b][br][off+cp : off+cp+N] into

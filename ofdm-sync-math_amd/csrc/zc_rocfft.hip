@@ -17,12 +17,40 @@
 #include <stdint.h>
 #include <math.h>
 #include <mutex>
+#include <string.h>
 #include "ofdmsync.h"
 
 namespace {
 
 constexpr int ZB = 64;          // max template bins (one lane each)
 constexpr int ZWG = 256;        // 4 waves = 4 streams per workgroup
+
+// Pruned output (store callback): rocFFT hands every output element to zc_store_cb instead of
+// writing it; the callback keeps only the template bins, in a compact [n_windows][n_bins]
+// buffer, so the dense N-point spectrum never reaches HBM (2 x 8N -> 8N + 8 n_bins bytes per
+// window).  cbdata lives in device memory; slot[k] = template position of unshifted bin k or -1.
+struct ZcCbData {
+    void* compact;              // [n_windows][n_bins] c64 | c128
+    int32_t n_bins, log2N;
+    int16_t slot[4096];
+};
+
+__device__ void zc_store_cb_f32(void* data, size_t offset, float2 element, void* cbdata, void*) {
+    (void)data;
+    const ZcCbData* d = static_cast<const ZcCbData*>(cbdata);
+    const size_t k = offset & ((size_t(1) << d->log2N) - 1);
+    const int s = d->slot[k];
+    if (s >= 0) static_cast<float2*>(d->compact)[(offset >> d->log2N) * d->n_bins + s] = element;
+}
+__device__ void zc_store_cb_f64(void* data, size_t offset, double2 element, void* cbdata, void*) {
+    (void)data;
+    const ZcCbData* d = static_cast<const ZcCbData*>(cbdata);
+    const size_t k = offset & ((size_t(1) << d->log2N) - 1);
+    const int s = d->slot[k];
+    if (s >= 0) static_cast<double2*>(d->compact)[(offset >> d->log2N) * d->n_bins + s] = element;
+}
+__device__ void* zc_store_cb_f32_ptr = (void*)zc_store_cb_f32;
+__device__ void* zc_store_cb_f64_ptr = (void*)zc_store_cb_f64;
 
 struct ZcFftPlan {
     rocfft_plan plan = nullptr;
@@ -31,6 +59,10 @@ struct ZcFftPlan {
     int64_t n_windows = 0;
     int64_t in_dist = 0;
     size_t work_bytes = 0;
+    int32_t prune = 0;          // > 0: pruned output with this many bins (store callback)
+    ZcCbData* cb_dev = nullptr; // device copy of the callback data
+    ZcCbData* cb_host = nullptr;// pinned staging
+    void* cb_fn = nullptr;      // device address of the store callback
 };
 
 struct GatherArgs {
@@ -123,10 +155,19 @@ std::once_flag g_setup;
 
 extern "C" {
 
+int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, void** plan_out, size_t* work_bytes);
+
 int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                void** plan_out, size_t* work_bytes) {
+    return ofs_zc_fft_plan_create2(precision, N, n_windows, in_dist, 0, plan_out, work_bytes);
+}
+
+int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, void** plan_out, size_t* work_bytes) {
     if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || n_windows < 1 ||
-        in_dist < N)
+        in_dist < N || prune_bins < 0 || prune_bins > ZB ||
+        (prune_bins > 0 && (N > 4096 || (N & (N - 1)))))
         return OFS_EINVAL;
     *plan_out = nullptr;
     std::call_once(g_setup, [] { rocfft_setup(); });
@@ -152,6 +193,22 @@ int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, 
     p->N = N;
     p->n_windows = n_windows;
     p->in_dist = in_dist;
+    if (prune_bins > 0) {
+        p->prune = prune_bins;
+        bool ok = hipMalloc(&p->cb_dev, sizeof(ZcCbData)) == hipSuccess &&
+                  hipHostMalloc(&p->cb_host, sizeof(ZcCbData)) == hipSuccess &&
+                  (memset(p->cb_host, 0, sizeof(ZcCbData)), true) &&
+                  hipMemcpyFromSymbol(&p->cb_fn, precision == OFS_FP32 ? HIP_SYMBOL(zc_store_cb_f32_ptr)
+                                                                      : HIP_SYMBOL(zc_store_cb_f64_ptr),
+                                      sizeof(void*)) == hipSuccess && p->cb_fn;
+        if (!ok) {
+            if (p->cb_dev) hipFree(p->cb_dev);
+            if (p->cb_host) hipHostFree(p->cb_host);
+            rocfft_plan_destroy(p->plan);
+            delete p;
+            return OFS_EHIP;
+        }
+    }
     if (work_bytes) *work_bytes = p->work_bytes;
     *plan_out = p;
     return OFS_OK;
@@ -161,6 +218,8 @@ int32_t ofs_zc_fft_plan_destroy(void* plan) {
     ZcFftPlan* p = static_cast<ZcFftPlan*>(plan);
     if (!p) return OFS_OK;
     if (p->plan) rocfft_plan_destroy(p->plan);
+    if (p->cb_dev) hipFree(p->cb_dev);
+    if (p->cb_host) hipHostFree(p->cb_host);
     delete p;
     return OFS_OK;
 }
@@ -176,6 +235,7 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
     const int32_t want_fmt = p->precision == OFS_FP32 ? OFS_C64 : OFS_C128;
     if (in_fmt != want_fmt || p->N != N || p->in_dist != T || p->n_windows != B * (int64_t)n_br) return OFS_EINVAL;
     if (p->work_bytes && !work) return OFS_EINVAL;
+    if (p->prune && p->prune != n_bins) return OFS_EINVAL;
     if (T < (int64_t)N + cp) return OFS_ESHORT;
     if (B == 0) return OFS_OK;
     const int64_t n_off = T - ((int64_t)N + cp) + 1;
@@ -186,7 +246,7 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
     g.B = B;
     g.n_off = n_off;
     g.n_br = n_br;
-    g.N = N;
+    g.N = p->prune ? n_bins : N;                    // pruned: compact [window][n_bins] rows
     g.n_bins = n_bins;
     g.e_t = template_energy;
     g.metric = metric;
@@ -197,12 +257,36 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
         g.t_re[k] = template_bins[2 * k];
         g.t_im[k] = template_bins[2 * k + 1];
     }
+    if (p->prune) {
+        ZcCbData h{};
+        h.compact = spectrum;
+        h.n_bins = n_bins;
+        while ((1 << h.log2N) < N) ++h.log2N;
+        for (int k = 0; k < 4096; ++k) h.slot[k] = -1;
+        for (int k = 0; k < n_bins; ++k) {
+            if (h.slot[g.pos[k]] >= 0) return OFS_EINVAL;             // duplicate bins: not prunable
+            h.slot[g.pos[k]] = (int16_t)k;
+            g.pos[k] = k;
+        }
+        // upload only when the table or the output buffer changed (steady state: no host sync)
+        if (memcmp(&h, p->cb_host, sizeof(ZcCbData)) != 0) {
+            if (hipStreamSynchronize(st) != hipSuccess) return OFS_EHIP;   // staging may feed a copy
+            memcpy(p->cb_host, &h, sizeof(ZcCbData));
+            if (hipMemcpyAsync(p->cb_dev, p->cb_host, sizeof(ZcCbData), hipMemcpyHostToDevice, st) != hipSuccess)
+                return OFS_EHIP;
+        }
+    }
 
     rocfft_execution_info info = nullptr;
     if (rocfft_execution_info_create(&info) != rocfft_status_success) return OFS_EFFT;
     rocfft_status s = rocfft_execution_info_set_stream(info, st);
     if (s == rocfft_status_success && p->work_bytes)
         s = rocfft_execution_info_set_work_buffer(info, work, p->work_bytes);
+    if (s == rocfft_status_success && p->prune) {
+        void* fns[1] = {p->cb_fn};
+        void* dat[1] = {p->cb_dev};
+        s = rocfft_execution_info_set_store_callback(info, fns, dat, 0);
+    }
     const size_t esz = p->precision == OFS_FP32 ? 8 : 16;
     const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
     int32_t rc = OFS_OK;

@@ -93,17 +93,20 @@ def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, te
 # full spectrum, so it is the comparison path for the fused window-FFT kernel above.
 # ------------------------------------------------------------------------------------------
 class FFTPlan:
-    """Caller-owned rocFFT plan for ``n_windows`` windows of ``N`` samples at distance ``T``."""
+    """Caller-owned rocFFT plan for ``n_windows`` windows of ``N`` samples at distance ``T``.
+    ``prune_bins`` > 0: pruned output (rocFFT store callback keeps only the template bins; the
+    spectrum buffer is then [n_windows][prune_bins])."""
 
-    def __init__(self, precision: int, N: int, n_windows: int, T: int):
+    def __init__(self, precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0):
         import ctypes
         self._lib = _lib.lib()
         h = ctypes.c_void_p()
         wb = ctypes.c_size_t()
-        _lib.check(self._lib.ofs_zc_fft_plan_create(int(precision), int(N), int(n_windows), int(T),
-                                                   ctypes.byref(h), ctypes.byref(wb)), "ofs_zc_fft_plan_create")
+        _lib.check(self._lib.ofs_zc_fft_plan_create2(int(precision), int(N), int(n_windows), int(T), int(prune_bins),
+                                                    ctypes.byref(h), ctypes.byref(wb)), "ofs_zc_fft_plan_create2")
         self.handle, self.work_bytes = h.value, int(wb.value)
-        self.key = (int(precision), int(N), int(n_windows), int(T))
+        self.prune_bins = int(prune_bins)
+        self.key = (int(precision), int(N), int(n_windows), int(T), int(prune_bins))
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
@@ -114,23 +117,25 @@ class FFTPlan:
 _plans: dict = {}
 
 
-def _plan(precision: int, N: int, n_windows: int, T: int) -> FFTPlan:
-    key = (precision, N, n_windows, T)
+def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0) -> FFTPlan:
+    key = (precision, N, n_windows, T, prune_bins)
     p = _plans.get(key)
     if p is None:
         if len(_plans) >= 8:
             _plans.clear()
-        p = _plans[key] = FFTPlan(precision, N, n_windows, T)
+        p = _plans[key] = FFTPlan(precision, N, n_windows, T, prune_bins)
     return p
 
 
 def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                             N: int | None = None, cp: int | None = None, *,
-                                            return_peak: bool = False):
+                                            return_peak: bool = False, pruned: bool = True):
     """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
     batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
     complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
-    per-stream ``peak_index`` (int64, np.argmax of zc_freq.py:144) and peak value (f64)."""
+    per-stream ``peak_index`` (int64, np.argmax of zc_freq.py:144) and peak value (f64).
+    ``pruned`` (default; N a power of two <= 4096, distinct bins): rocFFT's store callback keeps
+    only the template bins, so no dense spectrum is written; False: the dense spectrum."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -153,8 +158,9 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
             return (out, torch.empty((0,), dtype=torch.int64, device=dev),
                     torch.empty((0,), dtype=torch.float64, device=dev))
         return out
-    plan = _plan(prec, N, batch.B * batch.nb, batch.T)
-    spec = torch.empty((batch.B * batch.nb, N), dtype=batch.data.dtype, device=dev)
+    pruned = bool(pruned) and N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
+    plan = _plan(prec, N, batch.B * batch.nb, batch.T, int(idx.size) if pruned else 0)
+    spec = torch.empty((batch.B * batch.nb, int(idx.size) if pruned else N), dtype=batch.data.dtype, device=dev)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
     out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
     pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None

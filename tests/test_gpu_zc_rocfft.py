@@ -119,3 +119,20 @@ def test_row_argmax_numpy_semantics(dtype):
             assert vv[b] == v[b, ref[b]]
     idx1, _ = zc_freq.peak_index_batched(torch.tensor([[2.0]], dtype=dtype).cuda())
     assert int(idx1[0]) == 0
+
+
+@pytest.mark.parametrize("prec,N,cp,T,nb", [("c128", 256, 32, 700, 2), ("c64", 4096, 0, 4096, 1), ("c64", 2048, 0, 2300, 2)])
+def test_pruned_store_callback_equals_dense(prec, N, cp, T, nb):
+    """The pruned plan (rocFFT store callback keeping the 62 template bins) gives the dense plan's
+    metric: same transform, only the write of the unused bins is skipped."""
+    rng = np.random.default_rng(N + T)
+    B = 9
+    x = rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))
+    xd = torch.from_numpy(x.astype(np.complex128 if prec == "c128" else np.complex64)).cuda()
+    idx, t, e = zc_freq.make_pss_frequency_template()
+    a, pa, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=True)
+    b, pb, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=False)
+    tol = 1e-12 if prec == "c128" else 1e-5
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=tol, atol=tol * 1e-3)
+    ref = np.stack([O.zc_freq_metric(x[k], N, cp, idx, t, e) for k in range(B)])
+    np.testing.assert_allclose(a.cpu().numpy(), ref, rtol=1e-9 if prec == "c128" else 2e-5, atol=1e-7 if prec == "c128" else 2e-5)

@@ -313,7 +313,7 @@ def cfg3_fp64(dev, st, steps, warmup):
                 bytes_per_sample="16 in + P 16 + R 8 + M 8")
 
 
-def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5):
+def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5, pruned=None):
     """cfg5 through the rocFFT leg (ofs_zc_freq_metric_fft: batched rocFFT of every window into a
     dense spectrum, then the HIP gather/metric kernel and the per-sequence argmax), same input as
     cfg5.  alg_bytes counts the same 8 B/sample + output as cfg5 so Msamples/s and frac compare
@@ -324,22 +324,29 @@ def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5):
     for i in range(0, n_seq, 1 << 17):
         x[i:i + (1 << 17)].copy_(torch.randn((min(1 << 17, n_seq - i), N), dtype=torch.complex64, device=dev,
                                              generator=g))
-    spec = torch.empty((n_seq, N), dtype=torch.complex64, device=dev)
-    out = torch.empty((n_seq, 1), dtype=torch.float32, device=dev)
-    pk = torch.empty((n_seq,), dtype=torch.int64, device=dev)
+    if pruned is None:
+        pruned = os.environ.get("OFS_CFG5_DENSE", "0") != "1"
     idx, t, e = zc_freq.make_pss_frequency_template()
     idx32 = np.ascontiguousarray(idx.astype(np.int32))
     tb = np.ascontiguousarray(t.astype(np.complex128))
-    plan = zc_freq.FFTPlan(_lib.FP32, N, n_seq, N)
+    nb_ = len(idx32)
+    spec = torch.empty((n_seq, nb_ if pruned else N), dtype=torch.complex64, device=dev)
+    out = torch.empty((n_seq, 1), dtype=torch.float32, device=dev)
+    pk = torch.empty((n_seq,), dtype=torch.int64, device=dev)
+    plan = zc_freq.FFTPlan(_lib.FP32, N, n_seq, N, nb_ if pruned else 0)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
     L_ = _lib.lib()
     args = (plan.handle, _lib.C64, x.data_ptr(), n_seq, 1, N, N, 0, 62, idx32.ctypes.data, tb.ctypes.data, e,
             spec.data_ptr(), _lib.ptr(work), out.data_ptr(), pk.data_ptr(), None, st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_zc_freq_metric_fft(*args), "zc_freq rocfft"), steps, warmup, st)
-    return dict(config="cfg5_rocfft", workload=f"zc_freq 62-bin metric via rocFFT, N={N}, cp=0, {n_seq} sequences x {N} c64",
-                kernel="rocFFT fp32 C2C (batched, out-of-place) + zc_gather_kernel + row_argmax_kernel",
+    return dict(config="cfg5_rocfft" if pruned else "cfg5_rocfft_dense",
+                workload=f"zc_freq 62-bin metric via rocFFT, N={N}, cp=0, {n_seq} sequences x {N} c64",
+                kernel=("rocFFT fp32 C2C + pruning store callback (template bins only) + zc_gather_kernel + "
+                        "row_argmax_kernel" if pruned else
+                        "rocFFT fp32 C2C (batched, out-of-place, dense spectrum) + zc_gather_kernel + row_argmax_kernel"),
                 samples=n_seq * N, ms=ms, alg_bytes=n_seq * (N * 8 + 4),
-                traffic_bytes=n_seq * (2 * N * 8 + 62 * 8 + 4 + 8),
+                traffic_bytes=(n_seq * (N * 8 + 2 * 62 * 8 + 4 + 8) if pruned else
+                               n_seq * (2 * N * 8 + 62 * 8 + 4 + 8)),
                 bytes_per_sample="8 in + 4 B per sequence out (as cfg5); spectrum write + gather on top")
 
 
@@ -432,13 +439,15 @@ def aa_refshape_c128(dev, st, steps, warmup):
                    "sync_aa S&C fp64 L=512, 16384 x 2 ant x 5315 c128 (reference run_single_test shape)", 43)
 
 
-CONFIGS = {"cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
+CONFIGS = {"cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
+           "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
 # strong-scaled configs: global batch and the keyword that receives the rank's shard
-SHARDED = {"cfg4": ("cfg4_global", "B"), "cfg5": ("cfg5_global", "n_seq"), "cfg5_rocfft": ("cfg5_global", "n_seq")}
+SHARDED = {"cfg4": ("cfg4_global", "B"), "cfg5": ("cfg5_global", "n_seq"), "cfg5_rocfft": ("cfg5_global", "n_seq"),
+           "cfg5_rocfft_dense": ("cfg5_global", "n_seq")}
 
 
 def main(argv=None):
