@@ -129,13 +129,15 @@ def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0) -
 
 def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                             N: int | None = None, cp: int | None = None, *,
-                                            return_peak: bool = False, pruned: bool = True):
+                                            return_peak: bool = False, pruned: bool = False):
     """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
     batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
     complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
     per-stream ``peak_index`` (int64, np.argmax of zc_freq.py:144) and peak value (f64).
-    ``pruned`` (default; N a power of two <= 4096, distinct bins): rocFFT's store callback keeps
-    only the template bins, so no dense spectrum is written; False: the dense spectrum."""
+    ``pruned`` (N a power of two <= 4096, distinct bins): rocFFT's store callback keeps only the
+    template bins, so no dense spectrum is written (1.03x the algorithmic bytes instead of 2.02x);
+    measured 2.3x SLOWER on cfg5 (34.2 vs 15.0 ms: rocFFT's callback kernel calls the store
+    through a function pointer per element), hence off by default."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)

@@ -33,6 +33,7 @@ import torch  # noqa: E402
 from ofdm_sync_amd import _lib, shard, synth, zc_freq  # noqa: E402
 
 HBM = 8000.0
+VPEAK = {"fp32": 157.3, "fp64": 78.6}    # MI355X vector FMA peaks, TFLOP/s (spec; no MFMA: no contraction)
 _DIST = None                     # torch.distributed when run with N ranks (barrier before timing)
 
 
@@ -325,7 +326,7 @@ def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5, pruned=None):
         x[i:i + (1 << 17)].copy_(torch.randn((min(1 << 17, n_seq - i), N), dtype=torch.complex64, device=dev,
                                              generator=g))
     if pruned is None:
-        pruned = os.environ.get("OFS_CFG5_DENSE", "0") != "1"
+        pruned = True
     idx, t, e = zc_freq.make_pss_frequency_template()
     idx32 = np.ascontiguousarray(idx.astype(np.int32))
     tb = np.ascontiguousarray(t.astype(np.complex128))
@@ -439,7 +440,82 @@ def aa_refshape_c128(dev, st, steps, warmup):
                    "sync_aa S&C fp64 L=512, 16384 x 2 ant x 5315 c128 (reference run_single_test shape)", 43)
 
 
-CONFIGS = {"cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
+# ---- vector-FMA-bound kernels (Park, ZC matched filter, zc_freq sliding DFT) + the zc_v2 FSM ----
+def _flops(r, flops, prec):
+    r.update(alg_flops=flops, flop_prec=prec)
+    return r
+
+
+def park(dev, st, steps, warmup, prec="fp32"):
+    """park.park_streaming_metric (park.py:64-114), N = 2048: B = 2048 x T = 8192, one branch.
+    Direct sums per output d: P = Σ_{k<N/2} x[d-k]·x[d+k] (N/2 complex MACs = 4N flops) and
+    E = Σ_{k<N/2} |x[d+k]|² (N/2 x 2 FMA = 2N flops): 6N flops / output."""
+    from ofdm_sync_amd import park as pk
+    B, T, N = 2048, 8192, 2048
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn((B, 1, T), dtype=torch.complex64 if prec == "fp32" else torch.complex128, device=dev, generator=g)
+    ms = timed(lambda: pk.park_streaming_metric_batched(x, N, precision=prec), steps, warmup, st)
+    nout = T - 2 * (N // 2)
+    esz = 8 if prec == "fp32" else 16
+    return _flops(dict(config=f"park_{prec}", workload=f"park N={N}, {B} x {T} c{esz * 8}, {prec}",
+                       kernel=f"park_kernel<{prec}> (LDS tile, 8 outputs per thread)", samples=B * T, ms=ms,
+                       alg_bytes=B * T * esz + B * nout * (2 * esz + esz // 2 * 2), bytes_per_sample="in + P, E, M out"),
+                  B * nout * 6 * N, prec)
+
+
+def zc_mf(dev, st, steps, warmup):
+    """zc_v2 matched filter + normaliser (zc_v2.py:244-271, OFS_ZC_V2), 2048-tap PSS reference, fp64:
+    B = 512 x T = 16384 c128, outputs T + N - 1.  Per output: N complex MACs (8N flops) + the
+    sliding |x|² window (2 FMA)."""
+    from ofdm_sync_amd import zc_v2
+    B, T = 512, 16384
+    ref = zc_v2.build_pss_symbol(include_cp=False)
+    N = len(ref)
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randn((B, 1, T), dtype=torch.complex128, device=dev, generator=g)
+    ms = timed(lambda: zc_v2.correlate_batched(x, ref, zc_v2.OFS_ZC_V2, want_corr=True, want_mag=True), steps,
+               warmup, st)
+    nout = T + N - 1
+    return _flops(dict(config="zc_mf", workload=f"zc_v2 matched filter + normalise, N={N} taps, {B} x {T} c128, fp64",
+                       kernel="zc_mf_kernel<fp64> (direct correlation, LDS tile)", samples=B * T, ms=ms,
+                       alg_bytes=B * T * 16 + B * nout * 24, bytes_per_sample="16 in + corr 16 + |corr| 8 out"),
+                  B * nout * (8 * N + 4), "fp64")
+
+
+def zc_freq_fp64(dev, st, steps, warmup):
+    """zc_freq.compute_frequency_metric (zc_freq.py:62-99) at the reference's N = 2048, cp = 512, fp64
+    sliding DFT: B = 256 x T = 16384 c128.  Per offset and template bin: window update (x[s+N] -
+    x[s])·w^{ks} (6 + 2 flops), twiddle advance (6), vdot term (8): ~22 flops x 62 bins."""
+    B, T, N, cp = 256, 16384, 2048, 512
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn((B, 1, T), dtype=torch.complex128, device=dev, generator=g)
+    ms = timed(lambda: zc_freq.compute_frequency_metric_batched(x, N=N, cp=cp), steps, warmup, st)
+    noff = T - (N + cp) + 1
+    return _flops(dict(config="zc_freq_fp64", workload=f"zc_freq N={N} cp={cp}, {B} x {T} c128, fp64 sliding DFT",
+                       kernel="zc_freq_kernel<fp64> (lane = bin, sliding DFT)", samples=B * T, ms=ms,
+                       alg_bytes=B * T * 16 + B * noff * 8, bytes_per_sample="16 in + 8 out per offset"),
+                  B * noff * 62 * 22, "fp64")
+
+
+def zc_detect(dev, st, steps, warmup):
+    """zc_v2 CFAR + gate (zc_v2.py:300-446) on |corr| rows: B = 4096 x 16384 f64, sequential per
+    stream (one wave per stream, bit-exact left-to-right recursion); state arrays not stored."""
+    from ofdm_sync_amd import zc_v2
+    B, n = 4096, 16384
+    g = torch.Generator(device=dev).manual_seed(7)
+    mag = torch.rand((B, n), dtype=torch.float64, device=dev, generator=g) * 0.5
+    mag[:, 5000:5100] += 2.0
+    ms = timed(lambda: zc_v2._detect_run(mag, zc_v2.CORR_WINDOW_SIZE, zc_v2.THRESH_VALUE, zc_v2.THRESH_FRAC_BITS,
+                                         zc_v2.MIN_CORR_MAG, 2048, zc_v2.HYSTERESIS, 4, want_state=False),
+               steps, warmup, st)
+    return dict(config="zc_detect", workload=f"zc_v2 CFAR + gate, {B} x {n} f64 |corr| (events + gate mask)",
+                kernel="zc_detect_kernel (one wave per stream, sequential recursion)", samples=B * n, ms=ms,
+                alg_bytes=B * n * (8 + 1), bytes_per_sample="8 in + gate 1 out")
+
+
+CONFIGS = {"park_fp32": park, "park_fp64": lambda *a, **k: park(*a, prec="fp64", **k), "zc_mf": zc_mf,
+           "zc_freq_fp64": zc_freq_fp64, "zc_detect": zc_detect,
+           "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
            "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
@@ -496,6 +572,10 @@ def main(argv=None):
             r.update(scaling="per-rank", n_gpus=info.world)
         r["ms"] = ms
         gbs = r["alg_bytes"] / (ms / 1e3) / 1e9
+        if "alg_flops" in r:
+            tf = r["alg_flops"] / (ms / 1e3) / 1e12
+            r.update(achieved_TFLOPs=round(tf, 2), vector_peak_TFLOPs=VPEAK[r["flop_prec"]],
+                     flop_frac=round(tf / VPEAK[r["flop_prec"]], 4))
         r.update(value=round(r["samples"] / (ms / 1e3) / 1e6, 1), unit="Msamples/s",
                  ms=round(ms, 4), achieved_GBs=round(gbs, 1),
                  hbm_frac=round(gbs / (HBM * (info.world if name in SHARDED else 1)), 4),
