@@ -295,6 +295,22 @@ int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
                          const void* corr_in, void* corr, double* corr_mag, void* stream);
 
 /*
+ * The same correlation by FFT overlap-save (SURVEY §8(f)3 "via FFT correlation"): fp64 rocFFT
+ * transforms of M-sample blocks (M a power of two >= 2N, 0 = chosen to minimise the work),
+ * pointwise product with FFT_M(conj(ref reversed)), inverse, then the valid outputs combined
+ * and normalised per `mode` (OFS_ZC_RAW, _V2, _COMBINED, _SUM; as ofs_zc_correlate, the window
+ * energy from an fp64 prefix over each block; ref_energy as ofs_zc_correlate).  The plan is made
+ * for one reference (host c128, N taps) and one batch shape; `scratch` must hold *scratch_bytes (the [rows * blocks][M] c128
+ * spectra), `work` *work_bytes (rocFFT work area, may be 0).
+ */
+int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_br, int64_t T, int32_t M,
+                              void** plan_out, size_t* work_bytes, size_t* scratch_bytes);
+int32_t ofs_zc_mf_plan_destroy(void* plan);
+int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                             double ref_energy, int32_t mode, void* corr, double* corr_mag, void* scratch,
+                             void* work, void* stream);
+
+/*
  * ZC frequency-domain metric: replaces zc_freq.compute_frequency_metric (zc_freq.py:62-99).
  * For off in [0, T-(N+cp)]: 62-bin DFT of x[off+cp : off+cp+N] at fftshift positions
  * (N/2 + bin_indices) % N, metric = |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum|bins|^2, 1e-12).

@@ -1,0 +1,322 @@
+// zc_fftcorr.hip — the ZC matched filter through FFT overlap-save (SURVEY §8(f)3 "via FFT
+// correlation"): np.convolve(x, conj(ref[::-1]), 'full') of zc_v2.py:244-254 / zc.py:115-126
+// with a 2048-tap reference costs 2048 complex MACs per output as a direct sum (corr.hip,
+// zc_mf_kernel: fp64 vector-FMA bound); as overlap-save it is a few FFT passes per output.
+//
+//   block q of a row: u_q[m] = xz[q·S - (N-1) + m], m in [0, M)  (xz: x zero-padded), S = M - N + 1
+//   U = FFT_M(u_q) · H,  H = FFT_M(h),  h[i] = conj(ref[N-1-i]) zero-padded   (rocFFT, fp64)
+//   corr[q·S + s] = IFFT_M(U)[N - 1 + s] / M,  s in [0, S)
+//
+// Kernels: pack (rows x blocks into a [rows·nblk][M] c128 scratch), rocFFT forward (in place),
+// pointwise ·H, rocFFT inverse (in place), extract: per (stream, block) one workgroup reads the
+// valid part of every branch, combines the branches as the modes of ofs_zc_correlate (raw /
+// zc_v2 detect combine / zc.py combine / sum) and normalises with the sliding window energy
+// Σ|x|² over the same N samples, from an fp64 prefix scan of |u_q|² in LDS (error relative to
+// the block's energy, M = 4N samples).
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+#include <stdint.h>
+#include <math.h>
+#include <mutex>
+#include <algorithm>
+#include "ofdmsync.h"
+
+namespace {
+
+constexpr int FW = 256;
+
+struct McPlan {
+    rocfft_plan fwd = nullptr, inv = nullptr;
+    int32_t N = 0, M = 0, S = 0, nb = 0;
+    int64_t B = 0, T = 0, nblk = 0, nout = 0;
+    double2* H = nullptr;           // [M] FFT of the reversed conjugated reference
+    double ref_norm = 0.0;
+    size_t work_bytes = 0;
+    size_t scratch_bytes = 0;
+};
+
+std::once_flag g_setup;
+
+template <int FMT>
+__device__ __forceinline__ double2 ldx(const void* x, int64_t i) {
+    if constexpr (FMT == OFS_C64) {
+        const float2 v = static_cast<const float2*>(x)[i];
+        return make_double2(v.x, v.y);
+    } else if constexpr (FMT == OFS_C128) {
+        return static_cast<const double2*>(x)[i];
+    } else {
+        const short2 v = static_cast<const short2*>(x)[i];
+        return make_double2(v.x, v.y);
+    }
+}
+
+struct McArgs {
+    const void* x; int64_t T; int nb; int N, M, S; int64_t nblk, nout; int mode;
+    double ref_norm; double2* U; const double2* H; double2* out; double* mag;
+};
+
+// U[(row·nblk + q)][m] = xz_row[q·S - (N-1) + m]
+template <int FMT>
+__global__ __launch_bounds__(FW) void mc_pack_kernel(McArgs a) {
+    const int64_t blk = blockIdx.y;                 // row·nblk + q
+    const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+    const int64_t g0 = q * a.S - (a.N - 1);
+    double2* dst = a.U + blk * a.M;
+    for (int m = blockIdx.x * FW + threadIdx.x; m < a.M; m += gridDim.x * FW) {
+        const int64_t g = g0 + m;
+        dst[m] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, row * a.T + g) : make_double2(0.0, 0.0);
+    }
+}
+
+// U *= H / M (pointwise, every block)
+__global__ __launch_bounds__(FW) void mc_mul_kernel(double2* U, const double2* H, int64_t n, int M, double scale) {
+    for (int64_t i = blockIdx.x * (int64_t)FW + threadIdx.x; i < n; i += (int64_t)gridDim.x * FW) {
+        const double2 u = U[i], h = H[i % M];
+        U[i] = make_double2((u.x * h.x - u.y * h.y) * scale, (u.x * h.y + u.y * h.x) * scale);
+    }
+}
+
+// inclusive block scan of per-thread sums (fp64), returns the exclusive prefix of this thread
+__device__ double block_excl_scan(double v, double* red) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    double s = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(s, d, 64);
+        if (lane >= d) s += o;
+    }
+    if (lane == 63) red[w] = s;
+    __syncthreads();
+    double base = 0.0;
+    for (int j = 0; j < w; ++j) base += red[j];
+    __syncthreads();
+    return base + s - v;
+}
+
+// one workgroup per (stream, block): outputs n = q·S + s, s in [0, S) ∩ [0, nout - q·S).
+// LDS: the prefix of |u_q|^2 of every branch, [nb][M + 1] fp64, then the combine per output.
+template <int FMT>
+__global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
+    extern __shared__ double pf[];
+    double* red = pf + (size_t)a.nb * (a.M + 1);
+    const int64_t b = blockIdx.y, q = blockIdx.x;
+    const int64_t n0 = q * a.S;
+    const int ns = (int)min((int64_t)a.S, a.nout - n0);
+    const int per = (a.M + FW - 1) / FW;            // |u|^2 elements per thread in the scan
+    const int64_t g0 = n0 - (a.N - 1);
+    for (int br = 0; br < a.nb; ++br) {
+        const int64_t row = b * a.nb + br;
+        double* P = pf + (size_t)br * (a.M + 1);
+        double loc = 0.0;
+        for (int j = 0; j < per; ++j) {
+            const int m = threadIdx.x * per + j;
+            const int64_t g = g0 + m;
+            if (m < a.M && g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); loc += v.x * v.x + v.y * v.y; }
+        }
+        double run = block_excl_scan(loc, red);
+        for (int j = 0; j < per; ++j) {
+            const int m = threadIdx.x * per + j;
+            if (m < a.M) {
+                P[m] = run;
+                const int64_t g = g0 + m;
+                if (g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); run += v.x * v.x + v.y * v.y; }
+            }
+        }
+        if (threadIdx.x == FW - 1) P[a.M] = run;
+    }
+    __syncthreads();
+    for (int s = threadIdx.x; s < ns; s += FW) {
+        double sr = 0.0, si = 0.0, se = 0.0;
+        for (int br = 0; br < a.nb; ++br) {
+            const int64_t row = b * a.nb + br;
+            const double2 c = a.U[(row * a.nblk + q) * a.M + (a.N - 1) + s];
+            const double* P = pf + (size_t)br * (a.M + 1);
+            const double e = P[s + a.N] - P[s];              // Σ |x|^2 over the N-sample window
+            if (a.mode == OFS_ZC_RAW) {
+                const int64_t o = row * a.nout + n0 + s;
+                if (a.out) a.out[o] = c;
+                if (a.mag) a.mag[o] = hypot(c.x, c.y);
+                continue;
+            }
+            if (a.mode == OFS_ZC_V2) {                       // zc_v2.py:493-500 combine
+                const double d = a.ref_norm * sqrt(e > 1e-12 ? e : 1e-12);
+                sr += c.x / d; si += c.y / d;
+            } else {
+                sr += c.x; si += c.y; se += e;
+            }
+        }
+        if (a.mode == OFS_ZC_RAW) continue;
+        if (a.mode == OFS_ZC_COMBINED) {                     // zc.py:113-126
+            const double d = a.ref_norm * sqrt((se > 0.0 ? se : 0.0) + 1e-12);
+            sr /= d; si /= d;
+        }
+        const int64_t o = b * a.nout + n0 + s;
+        if (a.out) a.out[o] = make_double2(sr, si);
+        if (a.mag) a.mag[o] = hypot(sr, si);
+    }
+}
+
+size_t extract_lds(int nb, int M) { return ((size_t)nb * (M + 1) + FW / 64) * sizeof(double); }
+
+int pick_m(int N, int64_t T, int nb) {
+    // overlap-save FFT size: power of two >= 2N minimising the transformed elements nblk·M
+    // (ties: the smaller M), with every branch's energy prefix of a block in LDS
+    const int64_t nout = T + N - 1;
+    int best = 0;
+    int64_t cost = INT64_MAX;
+    for (int64_t M = 1; M <= (int64_t)1 << 16; M <<= 1) {
+        if (M < 2 * (int64_t)N || extract_lds(nb, (int)M) > 160 * 1024) continue;
+        const int64_t S = M - N + 1, nblk = (nout + S - 1) / S;
+        if (nblk * M < cost) { cost = nblk * M; best = (int)M; }
+    }
+    return best;
+}
+
+rocfft_status make_plan(rocfft_plan* p, rocfft_transform_type dir, int M, int64_t batch) {
+    const size_t len = (size_t)M;
+    return rocfft_plan_create(p, rocfft_placement_inplace, dir, rocfft_precision_double, 1, &len, (size_t)batch,
+                              nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_br, int64_t T, int32_t M,
+                              void** plan_out, size_t* work_bytes, size_t* scratch_bytes) {
+    if (!ref || !plan_out || N < 1 || B < 1 || n_br < 1 || T < 1 || M < 0 || (M && (M & (M - 1))) ||
+        (M && M < 2 * N))
+        return OFS_EINVAL;
+    *plan_out = nullptr;
+    if (!M) M = pick_m(N, T, n_br);
+    if (!M || extract_lds(n_br, M) > 160 * 1024) return OFS_ETOOLONG;
+    std::call_once(g_setup, [] { rocfft_setup(); });
+    McPlan* p = new McPlan;
+    p->N = N; p->M = M; p->S = M - N + 1; p->nb = n_br; p->B = B; p->T = T;
+    p->nout = T + N - 1;
+    p->nblk = (p->nout + p->S - 1) / p->S;
+    const int64_t batch = B * n_br * p->nblk;
+    p->scratch_bytes = (size_t)batch * M * sizeof(double2);
+    rocfft_status s = make_plan(&p->fwd, rocfft_transform_type_complex_forward, M, batch);
+    if (s == rocfft_status_success) s = make_plan(&p->inv, rocfft_transform_type_complex_inverse, M, batch);
+    size_t w1 = 0, w2 = 0;
+    if (s == rocfft_status_success) s = rocfft_plan_get_work_buffer_size(p->fwd, &w1);
+    if (s == rocfft_status_success) s = rocfft_plan_get_work_buffer_size(p->inv, &w2);
+    p->work_bytes = w1 > w2 ? w1 : w2;
+    // H = FFT_M(h), h[i] = conj(ref[N-1-i]) (host build, one batch-1 transform on the device)
+    double2* hh = nullptr;
+    rocfft_plan p1 = nullptr;
+    bool ok = s == rocfft_status_success && hipMalloc(&p->H, (size_t)M * sizeof(double2)) == hipSuccess &&
+              hipHostMalloc(&hh, (size_t)M * sizeof(double2)) == hipSuccess;
+    if (ok) {
+        const double2* r = static_cast<const double2*>(ref);
+        double nrm = 0.0;
+        for (int i = 0; i < M; ++i) hh[i] = make_double2(0.0, 0.0);
+        for (int i = 0; i < N; ++i) {
+            const double2 v = r[N - 1 - i];
+            hh[i] = make_double2(v.x, -v.y);
+            nrm += v.x * v.x + v.y * v.y;
+        }
+        p->ref_norm = sqrt(nrm);
+        ok = hipMemcpy(p->H, hh, (size_t)M * sizeof(double2), hipMemcpyHostToDevice) == hipSuccess &&
+             make_plan(&p1, rocfft_transform_type_complex_forward, M, 1) == rocfft_status_success;
+    }
+    if (ok) {
+        size_t w = 0;
+        void* wk = nullptr;
+        rocfft_execution_info info = nullptr;
+        ok = rocfft_plan_get_work_buffer_size(p1, &w) == rocfft_status_success &&
+             (w == 0 || hipMalloc(&wk, w) == hipSuccess) &&
+             rocfft_execution_info_create(&info) == rocfft_status_success &&
+             (w == 0 || rocfft_execution_info_set_work_buffer(info, wk, w) == rocfft_status_success);
+        void* io[1] = {p->H};
+        if (ok) ok = rocfft_execute(p1, io, nullptr, info) == rocfft_status_success && hipDeviceSynchronize() == hipSuccess;
+        if (info) rocfft_execution_info_destroy(info);
+        if (wk) (void)hipFree(wk);
+    }
+    if (p1) rocfft_plan_destroy(p1);
+    if (hh) (void)hipHostFree(hh);
+    if (!ok) {
+        if (p->fwd) rocfft_plan_destroy(p->fwd);
+        if (p->inv) rocfft_plan_destroy(p->inv);
+        if (p->H) (void)hipFree(p->H);
+        delete p;
+        return OFS_EFFT;
+    }
+    if (work_bytes) *work_bytes = p->work_bytes;
+    if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
+    *plan_out = p;
+    return OFS_OK;
+}
+
+int32_t ofs_zc_mf_plan_destroy(void* plan) {
+    McPlan* p = static_cast<McPlan*>(plan);
+    if (!p) return OFS_OK;
+    if (p->fwd) rocfft_plan_destroy(p->fwd);
+    if (p->inv) rocfft_plan_destroy(p->inv);
+    if (p->H) (void)hipFree(p->H);
+    delete p;
+    return OFS_OK;
+}
+
+int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
+                             double ref_energy, int32_t mode, void* corr, double* corr_mag, void* scratch,
+                             void* work, void* stream) {
+    McPlan* p = static_cast<McPlan*>(plan);
+    if (!p || !x || !scratch || (in_fmt != OFS_C64 && in_fmt != OFS_C128 && in_fmt != OFS_CI16) ||
+        B != p->B || n_br != p->nb || T != p->T || (!corr && !corr_mag) ||
+        (mode != OFS_ZC_RAW && mode != OFS_ZC_V2 && mode != OFS_ZC_COMBINED && mode != OFS_ZC_SUM) ||
+        (p->work_bytes && !work) || !(ref_energy >= 0.0))
+        return OFS_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    McArgs a{x, T, n_br, p->N, p->M, p->S, p->nblk, p->nout, mode, sqrt(ref_energy), static_cast<double2*>(scratch),
+             p->H, static_cast<double2*>(corr), corr_mag};
+    const int64_t rows = B * n_br;
+    const dim3 gp((unsigned)((p->M + FW - 1) / FW), (unsigned)(rows * p->nblk));
+    switch (in_fmt) {
+        case OFS_C64: hipLaunchKernelGGL(mc_pack_kernel<OFS_C64>, gp, dim3(FW), 0, st, a); break;
+        case OFS_C128: hipLaunchKernelGGL(mc_pack_kernel<OFS_C128>, gp, dim3(FW), 0, st, a); break;
+        default: hipLaunchKernelGGL(mc_pack_kernel<OFS_CI16>, gp, dim3(FW), 0, st, a); break;
+    }
+    if (hipGetLastError() != hipSuccess) return OFS_EHIP;
+    rocfft_execution_info info = nullptr;
+    if (rocfft_execution_info_create(&info) != rocfft_status_success) return OFS_EFFT;
+    rocfft_status s = rocfft_execution_info_set_stream(info, st);
+    if (s == rocfft_status_success && p->work_bytes) s = rocfft_execution_info_set_work_buffer(info, work, p->work_bytes);
+    void* io[1] = {scratch};
+    if (s == rocfft_status_success) s = rocfft_execute(p->fwd, io, nullptr, info);
+    if (s == rocfft_status_success) {
+        const int64_t n = rows * p->nblk * p->M;
+        hipLaunchKernelGGL(mc_mul_kernel, dim3((unsigned)std::min<int64_t>((n + FW - 1) / FW, 1 << 20)), dim3(FW), 0, st,
+                           static_cast<double2*>(scratch), p->H, n, p->M, 1.0 / (double)p->M);
+        if (hipGetLastError() != hipSuccess) { rocfft_execution_info_destroy(info); return OFS_EHIP; }
+        s = rocfft_execute(p->inv, io, nullptr, info);
+    }
+    rocfft_execution_info_destroy(info);
+    if (s != rocfft_status_success) return OFS_EFFT;
+    const size_t lds = extract_lds(n_br, p->M);
+    const dim3 ge((unsigned)p->nblk, (unsigned)B);
+    switch (in_fmt) {
+        case OFS_C64:
+            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C64>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return OFS_EHIP;
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FW), lds, st, a);
+            break;
+        case OFS_C128:
+            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C128>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return OFS_EHIP;
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FW), lds, st, a);
+            break;
+        default:
+            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_CI16>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return OFS_EHIP;
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FW), lds, st, a);
+            break;
+    }
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+}  // extern "C"

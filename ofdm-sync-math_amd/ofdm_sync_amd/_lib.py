@@ -101,6 +101,11 @@ def _declare(lib):
         "ofs_zc_fft_plan_destroy": (c_int32, [P]),
         "ofs_zc_freq_metric_fft": (c_int32, [P, c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,
                                              c_int32, P, P, c_double, P, P, P, P, P, P]),
+        "ofs_zc_mf_plan_create": (c_int32, [P, c_int32, c_int64, c_int32, c_int64, c_int32, P,
+                                            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
+        "ofs_zc_mf_plan_destroy": (c_int32, [P]),
+        "ofs_zc_correlate_fft": (c_int32, [P, c_int32, P, c_int64, c_int32, c_int64, c_double, c_int32, P, P, P,
+                                           P, P]),
         "ofs_row_argmax": (c_int32, [c_int32, P, c_int64, c_int64, P, P, P]),
         "ofs_zc_detect": (c_int32, [P, c_int64, c_int64, c_int32, c_int64, c_int32, c_double, c_int32,
                                     c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),

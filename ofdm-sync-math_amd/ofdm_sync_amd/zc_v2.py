@@ -98,8 +98,51 @@ def _ref_dev(reference, dev):
     return torch.from_numpy(np.ascontiguousarray(r)).to(dev), energy
 
 
-def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, want_mag=False):
-    """ofs_zc_correlate over x[B, n_branch, T] -> (corr, corr_mag) device tensors."""
+class MFPlan:
+    """FFT overlap-save matched-filter plan (ofs_zc_mf_plan_create) for one reference and one
+    batch shape [B, n_branch, T]; owns the rocFFT plans, the reference spectrum and scratch."""
+
+    def __init__(self, reference, B: int, nb: int, T: int, dev, M: int = 0):
+        import ctypes
+        r = np.ascontiguousarray(np.asarray(reference.cpu().numpy() if isinstance(reference, torch.Tensor)
+                                            else reference, dtype=np.complex128))
+        self._lib = _lib.lib()
+        h, wb, sb = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_size_t()
+        _lib.check(self._lib.ofs_zc_mf_plan_create(r.ctypes.data, r.size, int(B), int(nb), int(T), int(M),
+                                                  ctypes.byref(h), ctypes.byref(wb), ctypes.byref(sb)),
+                   "ofs_zc_mf_plan_create")
+        self.handle = h.value
+        self.key = (r.tobytes(), int(B), int(nb), int(T), int(M), str(dev))
+        self.scratch = torch.empty((max(int(sb.value), 1),), dtype=torch.uint8, device=dev)
+        self.work = torch.empty((int(wb.value),), dtype=torch.uint8, device=dev) if wb.value else None
+
+    def __del__(self):
+        h, self.handle = getattr(self, "handle", None), None
+        if h:
+            self._lib.ofs_zc_mf_plan_destroy(h)
+
+
+_mf_plans: dict = {}
+FFT_MIN_TAPS = 256          # the FFT path from this reference length on (direct sums below)
+
+
+def _mf_plan(reference, B, nb, T, dev) -> MFPlan:
+    r = np.asarray(reference.cpu().numpy() if isinstance(reference, torch.Tensor) else reference, np.complex128)
+    key = (r.tobytes(), int(B), int(nb), int(T), 0, str(dev))
+    p = _mf_plans.get(key)
+    if p is None:
+        if len(_mf_plans) >= 4:
+            _mf_plans.clear()
+        p = _mf_plans[key] = MFPlan(r, B, nb, T, dev)
+    return p
+
+
+def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, want_mag=False, method: str = "auto"):
+    """Correlation of x[B, n_branch, T] with `reference` -> (corr, corr_mag) device tensors.
+
+    method "direct": ofs_zc_correlate (O(N) MACs per output, fp64); "fft": ofs_zc_correlate_fft
+    (overlap-save through rocFFT, fp64); "auto": the FFT path for references of >= FFT_MIN_TAPS
+    taps (measured 2048 taps: DESIGN.md §4.5b) in every mode but OFS_ZC_NORMALIZE."""
     batch = _lib.as_batch(x, batched=True)
     dev = batch.data.device
     ref, energy = _ref_dev(reference, dev)
@@ -108,6 +151,17 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     shape = (batch.B, batch.nb, nout) if mode == OFS_ZC_RAW else (batch.B, nout)
     corr = torch.empty(shape, dtype=torch.complex128, device=dev) if want_corr else None
     mag = torch.empty(shape, dtype=torch.float64, device=dev) if want_mag else None
+    if method not in ("auto", "direct", "fft"):
+        raise ValueError("method must be 'auto', 'direct' or 'fft'")
+    use_fft = mode != OFS_ZC_NORMALIZE and batch.B > 0 and batch.T > 0 and (
+        method == "fft" or (method == "auto" and N >= FFT_MIN_TAPS))
+    if use_fft:
+        plan = _mf_plan(ref, batch.B, batch.nb, batch.T, dev)
+        rc = _lib.lib().ofs_zc_correlate_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
+                                             batch.T, energy, int(mode), _lib.ptr(corr), _lib.ptr(mag),
+                                             plan.scratch.data_ptr(), _lib.ptr(plan.work), _lib.stream_ptr())
+        _lib.check(rc, "ofs_zc_correlate_fft")
+        return corr, mag
     ci = None
     if mode == OFS_ZC_NORMALIZE:
         ci = torch.as_tensor(corr_in).to(device=dev, dtype=torch.complex128).reshape(batch.B, nout).contiguous()
