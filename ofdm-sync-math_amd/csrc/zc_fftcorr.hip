@@ -94,44 +94,51 @@ __device__ double block_excl_scan(double v, double* red) {
 }
 
 // one workgroup per (stream, block): outputs n = q·S + s, s in [0, S) ∩ [0, nout - q·S).
-// LDS: the prefix of |u_q|^2 of every branch, [nb][M + 1] fp64, then the combine per output.
+// LDS: per branch the exclusive prefix of |u_q|^2 over the block, [M + FW + 1] fp64 with one
+// pad word per `per` = M / FW elements (thread t scans the contiguous chunk [t·per, (t+1)·per),
+// padded so the chunk starts fall on different banks); x is read once, coalesced.
+__device__ __forceinline__ int pidx(int m, int per) { return m + m / per; }
+
 template <int FMT>
 __global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
     extern __shared__ double pf[];
-    double* red = pf + (size_t)a.nb * (a.M + 1);
+    const int per = a.M / FW;                       // M is a power of two >= FW
+    const int plen = a.M + FW + 1;                  // padded prefix length per branch (M / per = FW pads)
+    double* red = pf + (size_t)a.nb * plen;
     const int64_t b = blockIdx.y, q = blockIdx.x;
     const int64_t n0 = q * a.S;
     const int ns = (int)min((int64_t)a.S, a.nout - n0);
-    const int per = (a.M + FW - 1) / FW;            // |u|^2 elements per thread in the scan
     const int64_t g0 = n0 - (a.N - 1);
     for (int br = 0; br < a.nb; ++br) {
         const int64_t row = b * a.nb + br;
-        double* P = pf + (size_t)br * (a.M + 1);
-        double loc = 0.0;
-        for (int j = 0; j < per; ++j) {
-            const int m = threadIdx.x * per + j;
+        double* P = pf + (size_t)br * plen;
+        for (int m = threadIdx.x; m < a.M; m += FW) {            // |x|^2, coalesced
             const int64_t g = g0 + m;
-            if (m < a.M && g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); loc += v.x * v.x + v.y * v.y; }
+            double e = 0.0;
+            if (g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); e = v.x * v.x + v.y * v.y; }
+            P[pidx(m, per)] = e;
         }
+        __syncthreads();
+        const int c0 = threadIdx.x * per;
+        double loc = 0.0;
+        for (int j = 0; j < per; ++j) loc += P[pidx(c0 + j, per)];
         double run = block_excl_scan(loc, red);
         for (int j = 0; j < per; ++j) {
-            const int m = threadIdx.x * per + j;
-            if (m < a.M) {
-                P[m] = run;
-                const int64_t g = g0 + m;
-                if (g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); run += v.x * v.x + v.y * v.y; }
-            }
+            const int i = pidx(c0 + j, per);
+            const double e = P[i];
+            P[i] = run;
+            run += e;
         }
-        if (threadIdx.x == FW - 1) P[a.M] = run;
+        if (threadIdx.x == FW - 1) P[pidx(a.M, per)] = run;
+        __syncthreads();
     }
-    __syncthreads();
     for (int s = threadIdx.x; s < ns; s += FW) {
         double sr = 0.0, si = 0.0, se = 0.0;
         for (int br = 0; br < a.nb; ++br) {
             const int64_t row = b * a.nb + br;
             const double2 c = a.U[(row * a.nblk + q) * a.M + (a.N - 1) + s];
-            const double* P = pf + (size_t)br * (a.M + 1);
-            const double e = P[s + a.N] - P[s];              // Σ |x|^2 over the N-sample window
+            const double* P = pf + (size_t)br * plen;
+            const double e = P[pidx(s + a.N, per)] - P[pidx(s, per)];   // Σ |x|^2 over the N-sample window
             if (a.mode == OFS_ZC_RAW) {
                 const int64_t o = row * a.nout + n0 + s;
                 if (a.out) a.out[o] = c;
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
     }
 }
 
-size_t extract_lds(int nb, int M) { return ((size_t)nb * (M + 1) + FW / 64) * sizeof(double); }
+size_t extract_lds(int nb, int M) { return ((size_t)nb * (M + FW + 1) + FW / 64) * sizeof(double); }
 
 int pick_m(int N, int64_t T, int nb) {
     // overlap-save FFT size: power of two >= 2N minimising the transformed elements nblk·M
@@ -165,7 +172,7 @@ int pick_m(int N, int64_t T, int nb) {
     int best = 0;
     int64_t cost = INT64_MAX;
     for (int64_t M = 1; M <= (int64_t)1 << 16; M <<= 1) {
-        if (M < 2 * (int64_t)N || extract_lds(nb, (int)M) > 160 * 1024) continue;
+        if (M < 2 * (int64_t)N || M < FW || extract_lds(nb, (int)M) > 160 * 1024) continue;
         const int64_t S = M - N + 1, nblk = (nout + S - 1) / S;
         if (nblk * M < cost) { cost = nblk * M; best = (int)M; }
     }
@@ -185,7 +192,7 @@ extern "C" {
 int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_br, int64_t T, int32_t M,
                               void** plan_out, size_t* work_bytes, size_t* scratch_bytes) {
     if (!ref || !plan_out || N < 1 || B < 1 || n_br < 1 || T < 1 || M < 0 || (M && (M & (M - 1))) ||
-        (M && M < 2 * N))
+        (M && (M < 2 * N || M < FW)))
         return OFS_EINVAL;
     *plan_out = nullptr;
     if (!M) M = pick_m(N, T, n_br);
