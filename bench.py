@@ -173,7 +173,23 @@ def cpu_baseline(det, L: int, threads: int, budget: float):
     out["per_core_Msamples_s"] = out["value"] / threads
     out["numpy"] = _pool_leg(xh, L, "numpy", threads, budget)
     out["literal_loop"] = _pool_leg(xh, L, "loop", threads, budget)
+    out["other_configs"] = other_config_baselines(threads, budget)
     return out, par
+
+
+def other_config_baselines(workers: int, budget: float):
+    """CPU rates of BASELINE.json's other configs: the NumPy restatement of each
+    config's path on seeded synthetic streams of its shape, pool of `workers` processes
+    (oracle/cpu_pool.py --config).  GPU rates of the same configs: tools/bench_configs.py."""
+    res = {}
+    for name in ("cfg2a", "cfg2b", "cfg4", "cfg5"):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_pool.py"), "--config", name,
+                            str(workers), str(budget)], capture_output=True, text=True, check=True)
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+        res[name] = dict(value=round(r["value"], 3), unit="Msamples/s", cores=workers, kind="port",
+                         sample=f"{r['streams']} streams x {r['samples'] // max(r['streams'], 1)} samples, {r['form']}, "
+                                f"pool of {workers} processes, {r['seconds']:.2f} s wall")
+    return res
 
 
 # ------------------------------------------------------------------------------------------
