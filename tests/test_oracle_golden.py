@@ -155,6 +155,8 @@ def test_oracle_matches_reference_golden(path):
         for j in range(4):
             r = O.streaming_peak(d["metric"], d[f"mask{j}"])
             assert (-1 if r is None else r) == int(d[f"peak{j}"])
+    elif kind == "synth":
+        pass        # input builders of the synthesis: pinned in tests/test_host_logic.py
     else:
         pytest.fail(kind)
 
