@@ -33,7 +33,7 @@ def test_gpus2_weak_launches_two_ranks():
     # rank 1 sleeps 4 ms per step, rank 0 2 ms: the reported time is rank 1's (MAX over ranks)
     assert r["ms_per_step"] >= 0.95 * 4.0
     assert r["ms_per_step"] * steps > r["rank_ms"]
-    assert r["value"] == pytest.approx(2 * 64 * 1024 * steps / (r["ms_per_step"] * steps / 1e3) / 1e6, rel=1e-3)
+    assert r["value"] == pytest.approx(2 * 64 * 1024 * steps / (r["ms_per_step"] * steps / 1e3) / 1e6, abs=0.11)
 
 
 @pytest.mark.timeout(300)
