@@ -186,6 +186,164 @@ int oracle_aa_detect(const void* x, int is_c128, int64_t B, int64_t na, int64_t 
     return rc;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * minn_rtl: statement-for-statement restatement of minn_rtl._DelayLine (minn_rtl.py:512-542),
+ * _RunningSum (:545-580), _antenna_path (:583-652), minn_rtl_streaming_metric (:667-733, float
+ * smoothing) and detect_minn_rtl (:750-825).  x: [B][nb][T] complex128 (re, im interleaved).
+ * Outputs (each [B][T], nullable): corr_total, corr_positive, smooth, energy_total, corr_scaled,
+ * energy_scaled (f64), metric_valid, above (u8); events [B][max_ev][4] int64 = (peak_index,
+ * detected_index, seg_start, seg_end); n_ev [B]; open_start [B] (-1: none).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct { double* mem; int64_t depth, wr, fill; double last; } rtl_delay;
+typedef struct { double* mem; int64_t depth, wr, fill; double sum; int valid; } rtl_rsum;
+
+static double rtl_delay_step(rtl_delay* d, double v, int in_valid, int* out_valid) {
+    if (d->depth == 0) { if (in_valid) d->last = v; *out_valid = in_valid; return v; }
+    if (!in_valid) { *out_valid = 0; return d->last; }
+    const double rd = d->fill < d->depth ? 0.0 : d->mem[d->wr];
+    d->mem[d->wr] = v;
+    d->wr = (d->wr + 1) % d->depth;
+    if (d->fill < d->depth) { d->fill++; d->last = 0.0; *out_valid = 0; return 0.0; }
+    d->last = rd; *out_valid = 1; return rd;
+}
+
+static double rtl_rsum_step(rtl_rsum* r, double v, int in_valid, int* out_valid) {
+    if (r->depth == 0) { if (in_valid) { r->sum = v; r->valid = 1; } *out_valid = r->valid; return r->sum; }
+    if (!in_valid) { *out_valid = r->valid; return r->sum; }
+    const double oldest = r->fill < r->depth ? 0.0 : r->mem[r->wr];
+    r->mem[r->wr] = v;
+    r->wr = (r->wr + 1) % r->depth;
+    r->sum = r->sum + v - oldest;
+    if (r->fill < r->depth) { r->fill++; if (r->fill >= r->depth) r->valid = 1; } else r->valid = 1;
+    *out_valid = r->valid;
+    return r->sum;
+}
+
+static void rtl_one(const double* x, int64_t nb, int64_t T, int64_t Q, int shift, int64_t thr, int frac,
+                    int hyst, int toff, int max_ev, double* ct, double* cpos, double* sm, double* et,
+                    double* cs, double* es, unsigned char* mv, unsigned char* ab, int64_t* ev, int32_t* n_ev,
+                    int64_t* open_start, double* w_ct, double* w_et, unsigned char* w_v, double* w_cp,
+                    unsigned char* w_ab) {
+    for (int64_t n = 0; n < T; ++n) { w_ct[n] = 0.0; w_et[n] = 0.0; w_v[n] = 1; }
+    double* buf = (double*)calloc((size_t)(7 * (Q > 0 ? Q : 1)), sizeof(double));
+    for (int64_t br = 0; br < nb; ++br) {
+        const double* xs = x + 2 * br * T;
+        rtl_delay di = {buf, Q, 0, 0, 0.0}, dq = {buf + Q, Q, 0, 0, 0.0};
+        rtl_rsum cw = {buf + 2 * Q, Q, 0, 0, 0.0, 0}, ew = {buf + 3 * Q, Q, 0, 0, 0.0, 0};
+        rtl_delay cd = {buf + 4 * Q, Q, 0, 0, 0.0}, e1 = {buf + 5 * Q, Q, 0, 0, 0.0}, e2 = {buf + 6 * Q, Q, 0, 0, 0.0};
+        memset(buf, 0, sizeof(double) * (size_t)(7 * Q));
+        double cr = 0.0, cp = 0.0, er = 0.0, ep = 0.0, ep2 = 0.0;
+        for (int64_t n = 0; n < T; ++n) {
+            const double in_i = xs[2 * n], in_q = xs[2 * n + 1];
+            int v0, v1, cv, ev_, cpv, eqv, e2v;
+            const double d_i = rtl_delay_step(&di, in_i, 1, &v0);
+            const double d_q = rtl_delay_step(&dq, in_q, 1, &v1);
+            const double qp = d_i * in_i + d_q * in_q;                       /* minn_rtl.py:616 */
+            const double pw = in_i * in_i + in_q * in_q;                     /* :617 */
+            const double csum = rtl_rsum_step(&cw, qp, 1, &cv);
+            const double esum = rtl_rsum_step(&ew, pw, 1, &ev_);
+            const double cpv_ = rtl_delay_step(&cd, csum, cv, &cpv);
+            const double eq = rtl_delay_step(&e1, esum, ev_, &eqv);
+            const double e2q = rtl_delay_step(&e2, eq, eqv, &e2v);
+            if (cv) cr = csum;
+            if (cpv) cp = cpv_;
+            if (ev_) er = esum;
+            if (eqv) ep = eq;
+            if (e2v) ep2 = e2q;
+            w_ct[n] += cr + cp;                                               /* :695-702 */
+            w_et[n] += er + ep + ep2;
+            w_v[n] = w_v[n] && e2v;
+        }
+    }
+    free(buf);
+    double s = 0.0;
+    const double denom = (double)(1LL << (shift > 0 ? shift : 0));
+    for (int64_t n = 0; n < T; ++n) {
+        const double c = w_ct[n] > 0.0 ? w_ct[n] : 0.0;                      /* :704 */
+        if (w_v[n]) s = (shift == 0) ? c : s + (c - s) / denom;              /* :709-715 */
+        const double c_s = s * (double)(1LL << frac);
+        const double e_s = thr == 0 ? 0.0 : w_et[n] * (double)thr;           /* :718-721 */
+        const int a = w_v[n] && (c_s >= e_s);
+        w_cp[n] = c; w_ab[n] = (unsigned char)a;
+        if (ct) ct[n] = w_ct[n];
+        if (cpos) cpos[n] = c;
+        if (sm) sm[n] = s;
+        if (et) et[n] = w_et[n];
+        if (cs) cs[n] = c_s;
+        if (es) es[n] = e_s;
+        if (mv) mv[n] = w_v[n];
+        if (ab) ab[n] = (unsigned char)a;
+    }
+    /* detect_minn_rtl (minn_rtl.py:750-825) */
+    int gate_open = 0, k = 0;
+    int64_t gs = -1, pk = 0, low = 0;
+    double pv = 0.0;
+    const int64_t limit = hyst > 0 ? hyst - 1 : 0;
+    for (int64_t n = 0; n < T; ++n) {
+        if (!w_v[n]) continue;
+        const double m = w_cp[n];
+        if (!gate_open) {
+            if (w_ab[n]) { gate_open = 1; gs = n; pv = m; pk = n; low = 0; }
+        } else {
+            if (m >= pv) { pv = m; pk = n; }
+            if (w_ab[n]) {
+                low = 0;
+            } else {
+                int closing = 0;
+                if (hyst == 0) closing = 1;
+                else if (low == limit) closing = 1;
+                else low++;
+                if (closing) {
+                    if (k < max_ev) {
+                        int64_t* e = ev + 4 * k;
+                        e[0] = pk; e[1] = pk + toff; e[2] = gs >= 0 ? gs : n; e[3] = n + 1;
+                    }
+                    k++;
+                    gate_open = 0; gs = -1; pv = 0.0; low = 0;
+                }
+            }
+        }
+    }
+    *n_ev = k;
+    *open_start = (gate_open && gs >= 0) ? gs : -1;
+}
+
+int oracle_minn_rtl(const double* x, int64_t B, int64_t nb, int64_t T, int64_t Q, int shift, int64_t thr,
+                    int frac, int hyst, int toff, int max_ev, double* ct, double* cpos, double* sm, double* et,
+                    double* cs, double* es, unsigned char* mv, unsigned char* ab, int64_t* ev, int32_t* n_ev,
+                    int64_t* open_start, int nthreads) {
+    if (!x || B < 0 || nb < 1 || T < 0 || Q < 1 || max_ev < 0 || !n_ev || !open_start) return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    int rc = 0;
+#pragma omp parallel
+    {
+        const size_t t1 = (size_t)(T > 0 ? T : 1);
+        double* w_ct = (double*)malloc(sizeof(double) * t1);
+        double* w_et = (double*)malloc(sizeof(double) * t1);
+        double* w_cp = (double*)malloc(sizeof(double) * t1);
+        unsigned char* w_v = (unsigned char*)malloc(t1);
+        unsigned char* w_ab = (unsigned char*)malloc(t1);
+        if (!w_ct || !w_et || !w_cp || !w_v || !w_ab) {
+#pragma omp atomic write
+            rc = -2;
+        }
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t b = 0; b < B; ++b) {
+            if (!w_ct || !w_et || !w_cp || !w_v || !w_ab) continue;
+            const int64_t o = b * T;
+#define RTL_P(p) ((p) ? (p) + o : NULL)
+            rtl_one(x + 2 * b * nb * T, nb, T, Q, shift, thr, frac, hyst, toff, max_ev, RTL_P(ct), RTL_P(cpos),
+                    RTL_P(sm), RTL_P(et), RTL_P(cs), RTL_P(es), RTL_P(mv), RTL_P(ab), ev + 4 * (int64_t)max_ev * b,
+                    n_ev + b, open_start + b, w_ct, w_et, w_v, w_cp, w_ab);
+#undef RTL_P
+        }
+        free(w_ct); free(w_et); free(w_cp); free(w_v); free(w_ab);
+    }
+    return rc;
+}
+
 int oracle_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -29,6 +29,10 @@ def lib():
                                        c_int, c_double, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                        c_void_p, c_void_p, c_int]
         l.oracle_max_threads.restype = c_int
+        l.oracle_minn_rtl.restype = c_int
+        l.oracle_minn_rtl.argtypes = [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int64, c_int, c_int,
+                                      c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int]
         _lib = l
     return _lib
 
@@ -56,6 +60,35 @@ def aa_detect(x, L, threshold=0.15, hysteresis=128, sample_rate=15.36e6, max_eve
     if rc:
         raise RuntimeError(f"oracle_aa_detect failed ({rc})")
     return dict(P=P, R=R, M=M, n_events=n_ev, ev_int=ev_i, ev_real=ev_r)
+
+
+def minn_rtl(x, Q, smooth_shift=3, threshold_value=3276, threshold_frac_bits=15, hysteresis=2,
+             timing_offset=0, max_events=16, nthreads=0):
+    """x: [B, nb, T] complex (host) -> dict of the minn_rtl state arrays + detect_minn_rtl events
+    (C restatement, float smoothing)."""
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.complex128))
+    if x.ndim == 2:
+        x = x[:, None, :]
+    B, nb, T = x.shape
+    f = lambda: np.empty((B, T))                  # noqa: E731
+    u = lambda: np.empty((B, T), np.uint8)        # noqa: E731
+    out = dict(corr_total=f(), corr_positive=f(), smooth_metric=f(), energy_total=f(), corr_scaled=f(),
+               energy_scaled=f(), metric_valid=u(), above_threshold=u())
+    ev = np.zeros((B, max(max_events, 1), 4), np.int64)
+    n_ev = np.zeros(B, np.int32)
+    og = np.zeros(B, np.int64)
+    o = out
+    rc = lib().oracle_minn_rtl(x.ctypes.data, B, nb, T, int(Q), int(smooth_shift), int(threshold_value),
+                               int(threshold_frac_bits), int(hysteresis), int(timing_offset), int(max_events),
+                               o["corr_total"].ctypes.data, o["corr_positive"].ctypes.data,
+                               o["smooth_metric"].ctypes.data, o["energy_total"].ctypes.data,
+                               o["corr_scaled"].ctypes.data, o["energy_scaled"].ctypes.data,
+                               o["metric_valid"].ctypes.data, o["above_threshold"].ctypes.data, ev.ctypes.data,
+                               n_ev.ctypes.data, og.ctypes.data, int(nthreads))
+    if rc:
+        raise RuntimeError(f"oracle_minn_rtl failed ({rc})")
+    out.update(events=ev, n_events=n_ev, open_gate_start=og)
+    return out
 
 
 def max_threads() -> int:

@@ -2,17 +2,21 @@
 size-independent properties plus oracle parity on sampled streams.
 
   cfg2  4096 x 1024 int12 streams: sync_aa L=128 and minn_rtl Q=64 on the integer-exact kernels,
-        bit-identical to the general engine (fp64, sequential IIR) on EVERY stream, the oracle on
-        a sample (exact integers);
+        bit-identical to the general engine (fp64, sequential IIR) AND to the C oracle (the
+        reference's streaming loops restated statement for statement) on EVERY stream: every
+        array bit for bit, every event;
+  cfg3  detect-only (events without P/R/M) on the full 65536 x 1024 batch: every stream's events
+        against the C oracle under oracle/parity.py's stated near-tie criterion;
   cfg4  32768 x 4096 c64 (one GPU's shard of 262144), fused combined S&C + Minn, N = 2048:
-        oracle on a sample (M 1e-6), combined S&C M <= 1/4 and Minn M >= 0 on every stream;
-  cfg5  262144 x 4096 c64 (a quarter of 1M; the full 32 GiB run is bench_configs' job),
-        zc_freq fp32 window FFT: oracle on a sample (2e-5 abs), 0 <= metric <= 1 everywhere.
+        oracle on 512 streams (M 1e-6), combined S&C M <= 1/4 and Minn M >= 0 on every stream;
+  cfg5  the full 1M x 4096 c64 batch (32 GiB), zc_freq fp32 window FFT: oracle on 4096 sequences
+        (2e-5 abs), 0 <= metric <= 1 on every sequence.
 """
 import numpy as np
 import pytest
 
 import ofdm_oracle as O
+import oracle_c
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -43,10 +47,17 @@ def test_cfg2_sync_aa_full_batch_exact(monkeypatch):
     live = (torch.arange(m, device=a.ev_int.device)[None, :] < a.n_events[:, None])[..., None]   # stored slots
     assert torch.equal(torch.where(live, a.ev_int[:, :m], 0), torch.where(live, g.ev_int[:, :m], 0))
     xi = x.cpu().numpy()
-    for b in np.linspace(0, B - 1, 6).astype(int):
-        xc = (xi[b, ..., 0] + 1j * xi[b, ..., 1]).astype(np.complex128)
-        P, R, M, v = O.aa_metric(xc, L)
-        assert np.array_equal(a.P[b].cpu().numpy(), P)
+    xc = (xi[..., 0] + 1j * xi[..., 1]).astype(np.complex128)                # [B, 2, T]
+    o = oracle_c.aa_detect(xc, L, max_events=int(a.ev_int.shape[1]), nthreads=16)
+    assert np.array_equal(a.P.cpu().numpy(), o["P"]) and np.array_equal(a.R.cpu().numpy(), o["R"])
+    np.testing.assert_allclose(a.M.cpu().numpy(), o["M"], rtol=1e-14, atol=0)   # hypot² vs re²+im²
+    assert np.array_equal(n, o["n_events"])
+    ei = a.ev_int.cpu().numpy()
+    er = a.ev_real.cpu().numpy()
+    for b in range(B):
+        k = min(int(n[b]), ei.shape[1])
+        assert np.array_equal(ei[b, :k], o["ev_int"][b, :k])
+        np.testing.assert_allclose(er[b, :k], o["ev_real"][b, :k], rtol=1e-12, atol=1e-9)
 
 
 def test_cfg2_minn_rtl_full_batch_exact(monkeypatch):
@@ -61,10 +72,19 @@ def test_cfg2_minn_rtl_full_batch_exact(monkeypatch):
               "metric_valid", "above_threshold", "n_events", "open_gate_start"):
         assert torch.equal(getattr(a, k), getattr(g, k)), k
     xi = x.cpu().numpy()
-    b = B // 3
-    xc = (xi[b, ..., 0] + 1j * xi[b, ..., 1]).astype(np.complex128)
-    s = O.minn_rtl_metric(xc, Q, minn_rtl.SMOOTH_SHIFT, minn_rtl.THRESH_VALUE, minn_rtl.THRESH_FRAC_BITS)
-    assert np.array_equal(a.smooth_metric[b].cpu().numpy(), s["smooth_metric"])
+    xc = (xi[..., 0] + 1j * xi[..., 1]).astype(np.complex128)
+    o = oracle_c.minn_rtl(xc, Q, minn_rtl.SMOOTH_SHIFT, minn_rtl.THRESH_VALUE, minn_rtl.THRESH_FRAC_BITS, 2, 0,
+                          max_events=int(a.events.shape[1]), nthreads=16)
+    for k in ("corr_total", "corr_positive", "smooth_metric", "energy_total", "corr_scaled", "energy_scaled"):
+        assert np.array_equal(getattr(a, k).cpu().numpy(), o[k]), k
+    assert np.array_equal(a.metric_valid.cpu().numpy(), o["metric_valid"].astype(bool))
+    assert np.array_equal(a.above_threshold.cpu().numpy(), o["above_threshold"].astype(bool))
+    n = a.n_events.cpu().numpy()
+    assert np.array_equal(n, o["n_events"]) and np.array_equal(a.open_gate_start.cpu().numpy(), o["open_gate_start"])
+    ev = a.events.cpu().numpy()
+    for b in range(B):
+        k = min(int(n[b]), ev.shape[1])
+        assert np.array_equal(ev[b, :k], o["events"][b, :k])
 
 
 def test_cfg4_fused_shard_full_size():
@@ -74,8 +94,8 @@ def test_cfg4_fused_shard_full_size():
     assert Ms.shape == (B, T - N + 1)
     assert bool(torch.isfinite(Ms).all()) and bool(torch.isfinite(Mm).all())
     assert float(Ms.max()) <= 0.25 + 1e-6 and float(Mm.min()) >= 0.0       # |P| <= (E1+E2)/2
-    xh = x[:: B // 8].cpu().numpy().astype(np.complex128)
-    for i, b in enumerate(range(0, B, B // 8)):
+    xh = x[:: B // 512].cpu().numpy().astype(np.complex128)
+    for i, b in enumerate(range(0, B, B // 512)):
         Mo, Po, Ro = O.comb_sc_metric(xh[i], N)
         assert np.max(np.abs(Ms[b].cpu().numpy() - Mo)) < 1e-6
         Mo, Po, Ro = O.minn_metric(xh[i], N)
@@ -83,10 +103,29 @@ def test_cfg4_fused_shard_full_size():
         assert np.all(np.abs(mm - Mo) <= 1e-6 * np.maximum(1.0, np.abs(Mo)))
 
 
-def test_cfg5_quarter_batch():
-    B, N = 262144, 4096
+def test_cfg3_detect_only_full_batch_vs_oracle():
+    """The headline batch with P/R/M not stored (SURVEY §8d detect-only): every stream's events
+    against the C oracle (oracle/parity.py: exact except stated near-ties; CFO angle <= 1e-6)."""
+    import parity
+    B, T, L = 65536, 1024, 512
+    x = synth.headline_batch(B, T, L, seed=777)
+    full = sync_aa.aa_detect_streaming_batched(x, L, outputs=("M",), max_events=8)
+    det = sync_aa.aa_detect_streaming_batched(x, L, outputs=(), max_events=8)
+    assert torch.equal(full.n_events, det.n_events)
+    o = oracle_c.aa_detect(x.cpu().numpy(), L, max_events=8, nthreads=16)
+    r = parity.classify_aa(full.M.cpu().numpy().astype(np.float64), det.n_events.cpu().numpy(),
+                           det.ev_int.cpu().numpy(), det.ev_real.cpu().numpy(), o["P"], o["M"], o["n_events"],
+                           o["ev_int"], o["ev_real"], L)
+    print("detect-only parity:", r)
+    assert r["mismatch"] == 0 and r["cfo_over_tol"] == 0 and r["events_engine"] == r["events_oracle"]
+
+
+def test_cfg5_full_batch():
+    B, N = 1 << 20, 4096
     g = torch.Generator(device="cuda").manual_seed(5)
-    x = torch.randn((B, N), dtype=torch.complex64, device="cuda", generator=g)
+    x = torch.empty((B, N), dtype=torch.complex64, device="cuda")
+    for i in range(0, B, 1 << 17):                       # 32 GiB, generated in chunks
+        x[i:i + (1 << 17)] = torch.randn((1 << 17, N), dtype=torch.complex64, device="cuda", generator=g)
     sym = torch.from_numpy(O.pss_symbol(N).astype(np.complex64)).cuda()
     x[::97] += 4.0 * sym                                                 # some windows carry the PSS
     idx, t, e = O.zc_template()
@@ -94,6 +133,6 @@ def test_cfg5_quarter_batch():
     assert m.shape == (B, 1)
     assert float(m.min()) >= 0.0 and float(m.max()) <= 1.0 + 1e-5        # Cauchy-Schwarz
     assert float(m[::97].min()) > 0.5
-    for b in list(range(0, B, B // 12)) + [97, 194]:
+    for b in list(range(0, B, B // 4096)) + [97, 194, B - 1]:
         mo = O.zc_freq_metric(x[b].cpu().numpy().astype(np.complex128)[None], N, 0, idx, t, e)
         assert abs(float(m[b, 0]) - mo[0]) < 2e-5

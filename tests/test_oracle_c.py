@@ -37,3 +37,21 @@ def test_c_oracle_batched_c64_threads():
     for b in (0, 17, 36):
         P, R, M, v = O.aa_metric(x[b].astype(np.complex128), 64)
         assert np.max(np.abs(r1["M"][b] - M)) < 1e-12
+
+
+RTL = [p for p in sorted(glob.glob(os.path.join(GOLDEN, "rtl_*.npz")))]
+
+
+@pytest.mark.parametrize("path", RTL, ids=lambda p: os.path.basename(p)[:-4])
+def test_c_minn_rtl_matches_reference_golden(path):
+    """The C restatement of minn_rtl's streaming pipeline + detect_minn_rtl (float smoothing)
+    reproduces the reference's arrays bit for bit and its events exactly."""
+    d = np.load(path)
+    r = oracle_c.minn_rtl(d["x"][None], int(d["Q"]), int(d["smooth_shift"]), int(d["threshold_value"]),
+                          int(d["threshold_frac_bits"]), int(d["hysteresis"]), int(d["timing_offset"]))
+    for k in ("corr_total", "corr_positive", "smooth_metric", "energy_total", "corr_scaled", "energy_scaled"):
+        assert np.array_equal(r[k][0], d[k]), k
+    assert np.array_equal(r["metric_valid"][0].astype(bool), d["metric_valid"])
+    assert np.array_equal(r["above_threshold"][0].astype(bool), d["above_threshold"])
+    n = int(r["n_events"][0])
+    assert np.array_equal(r["events"][0, :n], d["events"].reshape(-1, 4))
