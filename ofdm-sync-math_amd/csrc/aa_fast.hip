@@ -187,10 +187,10 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 #pragma unroll
             for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
             // ---- lane totals: fp64 DPP wave scan, row totals, rows inside the window ----
-            const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
-            const double totR = readlane(iR, 63), totI = readlane(iI, 63), totE = readlane(iE, 63);
-            const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);   // lanes < l
-            const float uR = (float)(totR - iR), uI = (float)(totI - iI), uE = (float)(totE - iE);  // lanes > l
+            const RowScan sRr = row_scan(fR[E - 1]), sIr = row_scan(fI[E - 1]), sEr = row_scan(fE[E - 1]);
+            const double totR = sRr.tot, totI = sIr.tot, totE = sEr.tot;
+            const float xR = sRr.x, xI = sIr.x, xE = sEr.x;             // lanes < l
+            const float uR = sRr.u, uI = sIr.u, uE = sEr.u;             // lanes > l
             Cr[k + 1] = Cr[k] + totR; Ci[k + 1] = Ci[k] + totI; Ce[k + 1] = Ce[k] + totE;
             const float wR = (float)((k >= MR) ? (Cr[k] - Cr[k - MR + 1]) : Cr[k]);
             const float wI = (float)((k >= MR) ? (Ci[k] - Ci[k - MR + 1]) : Ci[k]);
@@ -390,16 +390,16 @@ struct AaStream {
         gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
 #pragma unroll
         for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
-        const double iE = scan_add((double)fE[E - 1]);
-        const double tE = readlane(iE, 63);
-        const float xE = (float)shr1z(iE), uE = (float)(tE - iE);
-        double iR = 0.0, iI = 0.0, tR = 0.0, tI = 0.0;
+        const RowScan se_ = row_scan(fE[E - 1]);
+        const double tE = se_.tot;
+        const float xE = se_.x, uE = se_.u;
+        double tR = 0.0, tI = 0.0;
         float xR = 0.f, xI = 0.f, uR = 0.f, uI = 0.f;
         if (!FIRST) {                                        // no lagged product before row MR
-            iR = scan_add((double)fR[E - 1]); iI = scan_add((double)fI[E - 1]);
-            tR = readlane(iR, 63); tI = readlane(iI, 63);
-            xR = (float)shr1z(iR); xI = (float)shr1z(iI);
-            uR = (float)(tR - iR); uI = (float)(tI - iI);
+            const RowScan sr_ = row_scan(fR[E - 1]), si_ = row_scan(fI[E - 1]);
+            tR = sr_.tot; tI = si_.tot;
+            xR = sr_.x; xI = si_.x;
+            uR = sr_.u; uI = si_.u;
         }
         const float wR = (float)(FIRST ? CR : CR - cbR[so]);
         const float wI = (float)(FIRST ? CI : CI - cbI[so]);

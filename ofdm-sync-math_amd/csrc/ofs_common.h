@@ -173,6 +173,41 @@ __device__ __forceinline__ double scan_add(double v) {
 }
 __device__ __forceinline__ double shr1z(double v) { return dppz<0x138>(v); }   // wave_shr:1, lane 0 <- 0
 
+// the same ladder on floats (one v_add_f32 with a DPP source per step)
+template <int CTRL, int RMASK = 0xf>
+__device__ __forceinline__ float dppz_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, RMASK, 0xf, true));
+}
+__device__ __forceinline__ float scan_add_f32(float v) {
+    v += dppz_f<0x111>(v);
+    v += dppz_f<0x112>(v);
+    v += dppz_f<0x114>(v);
+    v += dppz_f<0x118>(v);
+    v += dppz_f<0x142, 0xa>(v);
+    v += dppz_f<0x143, 0xc>(v);
+    return v;
+}
+
+// Scan of one lane value across a row (the wave): x = sum over lanes < l, u = sum over lanes > l,
+// tot = the row total.  fp64 by default; OFS_SCAN32 (tuning builds) scans in fp32: the sums are
+// of one row's terms only (no cancellation against a stream-wide prefix), error ~6 ulp of the row.
+#ifndef OFS_SCAN32
+#define OFS_SCAN32 0
+#endif
+struct RowScan { float x, u; double tot; };
+__device__ __forceinline__ RowScan row_scan(float v) {
+#if OFS_SCAN32
+    const float i = scan_add_f32(v);
+    const float t = readlane(i, 63);
+    return RowScan{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(i), 0x138, 0xf, 0xf, true)), t - i,
+                   (double)t};
+#else
+    const double i = scan_add((double)v);
+    const double t = readlane(i, 63);
+    return RowScan{(float)shr1z(i), (float)(t - i), t};
+#endif
+}
+
 }  // namespace ofs
 
 // internal launchers implemented in aa_fast.hip (C++ linkage, not part of the ABI)

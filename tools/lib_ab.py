@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--detect-only", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="variants may differ in rounding (no bit-equality check)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, T, L, na, E = a.B, a.T, a.L, a.na, 4
@@ -66,7 +67,7 @@ def main():
             times[name].append(e0.elapsed_time(e1) / a.steps)
             if ref is None:
                 ref = (n_ev.clone(), None if M is None else M.clone())
-            else:
+            elif not a.no_check:
                 assert torch.equal(ref[0], n_ev), f"{name}: events differ"
                 if M is not None:
                     assert torch.equal(ref[1], M), f"{name}: M differs"

@@ -222,6 +222,13 @@ int main(int argc, char** argv) {
             report(nm, 40.0 * n, time_ms([&] { pattern_cfg4_f2<<<cus * grid_mult, 256>>>(x, (float2*)P1b, (float2*)R1b, (float2*)M1b,
                                                                                          (float2*)P2, (float2*)R2, (float2*)M2, n / 2); }, iters));
         }
+        report("pattern_cfg4(8r+32w, 16B stores) grid=full", 40.0 * n,
+               time_ms([&] { pattern_cfg4<<<(unsigned)((n / 4 + 255) / 256), 256>>>(x, P1b, R1b, M1b, P2, R2, M2, n / 4); }, iters));
+        report("pattern_cfg4_f2(8r+32w, misaligned 8B stores) grid=full", 40.0 * n,
+               time_ms([&] { pattern_cfg4_f2<<<(unsigned)((n / 2 + 255) / 256), 256>>>(x, (float2*)P1b, (float2*)R1b, (float2*)M1b,
+                                                                                         (float2*)P2, (float2*)R2, (float2*)M2, n / 2); }, iters));
+        report("write4 grid=full", 1.0 * n * 8,
+               time_ms([&] { write4<<<(unsigned)((n * 8 / 16 + 255) / 256), 256>>>(P1b, n * 8 / 16); }, iters));
         CK(hipFree(P2)); CK(hipFree(R2)); CK(hipFree(M2)); CK(hipFree(P1b)); CK(hipFree(R1b)); CK(hipFree(M1b));
     }
     report("pattern_wave(8r+16w) wave-per-stream again", 24.0 * n,
