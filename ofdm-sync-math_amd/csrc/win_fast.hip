@@ -216,6 +216,15 @@ struct WinFusedArgs {
     float* Ms; float2* Ps; float* Rs; float* Mm; float2* Pm; float* Rm;
 };
 
+// 16-byte-aligned output rows of the fused kernel (row origin shift).  Paired A/B (tools/lib_ab.py
+// --op scminn, r02r): 0.720 vs 0.711 ms on the cfg4 shard, 0.618 vs 0.576 ms with two branches -
+// slower than the misaligned 8-byte stores despite the flat SOL probe's 0.70 vs 0.60, so off.
+#ifndef OFS_SCM_ALIGN
+#define OFS_SCM_ALIGN 0
+#endif
+typedef float wf4u __attribute__((ext_vector_type(4), aligned(8)));
+typedef float wf2u __attribute__((ext_vector_type(2), aligned(4)));
+
 // occupancy bound (min waves per SIMD) of the fused kernel; tuning builds set -DOFS_SCM_WAVES=N
 #ifndef OFS_SCM_WAVES
 #define OFS_SCM_WAVES 0
@@ -242,7 +251,13 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
-    const int nrows = (int)((T + RL - 1) / RL);
+    // Row origin shift (OFS_SCM_ALIGN): the [B][T-N+1] output rows have odd length, so a lane's E
+    // outputs would start 4-byte-misaligned for 3 of 4 streams; starting the rows s samples
+    // before the stream (zeros there) puts every full lane group of outputs on a 16-byte boundary
+    // (flat SOL probe of this 1 : 4 read : write mix: 0.70 of peak with aligned 16-B stores
+    // against 0.60 with misaligned 8-B ones).  Inputs then load 8-byte-aligned (f4u).
+    const int64_t s = OFS_SCM_ALIGN ? (((b * nout - (N - 1)) % 4) + 4) % 4 : 0;
+    const int nrows = (int)((T + s + RL - 1) / RL);
     const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
 
     float xr_[NB][XR][E], xi_[NB][XR][E];
@@ -269,15 +284,29 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     auto H = [&](int row, int e) -> float& { return hist[w][row][e][lane]; };
 
     float4 nx[PD][NB][V4];
+    // row k = samples [RL·k - s, RL·(k+1) - s): pairs as 8-byte-aligned float4 when the row lies
+    // inside the stream, else per sample with zeros outside [0, T) (wave-uniform choice)
     auto load_row = [&](int k, float4 (&dst)[NB][V4]) {
+        const int64_t r0 = (int64_t)RL * k - s;
+        const int64_t n0 = r0 + E * lane;
+        const bool whole = r0 >= 0 && r0 + RL <= T;
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
-            const float4* xs = reinterpret_cast<const float4*>(xb + (int64_t)t * T);
+            const float2* xs = xb + (int64_t)t * T;
+            if (whole) {
 #pragma unroll
-            for (int j = 0; j < V4; ++j) {
-                const int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;
-                const int64_t qmax = T / 2 - 1;
-                dst[t][j] = xs[q < qmax ? q : qmax];
+                for (int j = 0; j < V4; ++j) {
+                    const wf4u v = *reinterpret_cast<const wf4u*>(xs + n0 + 2 * j);
+                    dst[t][j] = make_float4(v.x, v.y, v.z, v.w);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < V4; ++j) {
+                    const int64_t m0 = n0 + 2 * j, m1 = m0 + 1;
+                    const float2 u0 = (m0 >= 0 && m0 < T) ? xs[m0] : make_float2(0.f, 0.f);
+                    const float2 u1 = (m1 >= 0 && m1 < T) ? xs[m1] : make_float2(0.f, 0.f);
+                    dst[t][j] = make_float4(u0.x, u0.y, u1.x, u1.y);
+                }
             }
         }
     };
@@ -304,7 +333,7 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
         for (int u = 0; u < PER; ++u) {
             const int k = k0 + u;
             if (k < nrows) {
-                const int64_t nb = (int64_t)RL * k + E * lane;
+                const int64_t nb = (int64_t)RL * k + E * lane - s;
                 const int x2 = u % XR;                 // row k-2MW (x ring), then row k
                 const int x1 = (u + MW) % XR;          // row k-MW
                 float hR[E], hI[E], qR[E], qI[E], en[E];
@@ -314,11 +343,10 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
                 for (int t = 0; t < NB; ++t) {         // products summed over the branches
                     float cr[E], ci[E];
 #pragma unroll
-                    for (int j = 0; j < V4; ++j) {
-                        const bool ok = nb + 2 * j < T;
+                    for (int j = 0; j < V4; ++j) {     // zeros outside [0, T) come from load_row
                         const float4 v = nx[u % PD][t][j];
-                        cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
-                        cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
+                        cr[2 * j] = v.x; ci[2 * j] = v.y;
+                        cr[2 * j + 1] = v.z; ci[2 * j + 1] = v.w;
                     }
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
@@ -371,12 +399,30 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
                                const float (&pi)[E], const float (&r)[E]) {
                     Mo += b * nout; Po += b * nout; Ro += b * nout;
                     if (d0 >= 0 && d0 + E <= nout) {
+                        if constexpr (E >= 4) {
+                            if (OFS_SCM_ALIGN) {                   // 16-byte aligned (row shift s)
 #pragma unroll
-                        for (int j = 0; j < E; j += 2) {
-                            if (Mo) *reinterpret_cast<float2*>(Mo + d0 + j) = make_float2(m[j], m[j + 1]);
-                            if (Ro) *reinterpret_cast<float2*>(Ro + d0 + j) = make_float2(r[j], r[j + 1]);
-                            if (Po) *reinterpret_cast<float4*>(Po + d0 + j) = make_float4(pr[j], pi[j], pr[j + 1], pi[j + 1]);
+                                for (int j = 0; j < E; j += 4) {
+                                    if (Mo) *reinterpret_cast<float4*>(Mo + d0 + j) = make_float4(m[j], m[j + 1], m[j + 2], m[j + 3]);
+                                    if (Ro) *reinterpret_cast<float4*>(Ro + d0 + j) = make_float4(r[j], r[j + 1], r[j + 2], r[j + 3]);
+                                }
+                            } else {
+#pragma unroll
+                                for (int j = 0; j < E; j += 2) {
+                                    if (Mo) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{m[j], m[j + 1]};
+                                    if (Ro) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{r[j], r[j + 1]};
+                                }
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < E; j += 2) {
+                                if (Mo) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{m[j], m[j + 1]};
+                                if (Ro) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{r[j], r[j + 1]};
+                            }
                         }
+#pragma unroll
+                        for (int j = 0; j < E; j += 2)
+                            if (Po) *reinterpret_cast<wf4u*>(Po + d0 + j) = wf4u{pr[j], pi[j], pr[j + 1], pi[j + 1]};
                     } else {
 #pragma unroll
                         for (int e = 0; e < E; ++e) {

@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--detect-only", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="variants may differ in rounding (no bit-equality check)")
+    ap.add_argument("--op", choices=("aa", "scminn"), default="aa", help="aa: ofs_aa_detect; scminn: "
+                    "ofs_sc_minn_metric (cfg4 fused S&C + Minn, N = 2 L)")
     a = ap.parse_args()
+    if a.op == "scminn":
+        return scminn(a)
     dev = torch.device("cuda", 0)
     B, T, L, na, E = a.B, a.T, a.L, a.na, 4
     base = synth.faded_base(L, "cir1", tuple(range(na)) if na > 1 else (1,))
@@ -77,6 +81,46 @@ def main():
         print(json.dumps(dict(lib=name, shape=[B, na, T, L], plan=libs[0][1].ofs_aa_plan(_lib.C64, _lib.FP32, na, T, L),
                               ms_median=round(ms, 4), ms_all=[round(t, 4) for t in times[name]],
                               frac=round(alg / (ms / 1e3) / 8e12, 4))), flush=True)
+
+
+def scminn(a):
+    dev = torch.device("cuda", 0)
+    B, T, N, nb = a.B, a.T, 2 * a.L, a.na
+    x = synth.synth_batch(synth.faded_base(a.L, "cir1", tuple(range(nb)) if nb > 1 else (1,)), B, T, seed=4, device=dev)
+    nout = T - N + 1
+    outs = [torch.empty((B, nout), dtype=dt, device=dev) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    st = torch.cuda.current_stream(dev)
+    libs = []
+    for p in a.libs.split(","):
+        l = ctypes.CDLL(os.path.abspath(p))
+        _lib._declare(l)
+        libs.append((os.path.basename(p), l))
+    args = (_lib.C64, x.data_ptr(), B, nb, T, N, _lib.FP32, *[o.data_ptr() for o in outs], st.cuda_stream)
+    times = {n: [] for n, _ in libs}
+    ref = None
+    for r in range(a.rounds):
+        for name, l in libs[r % len(libs):] + libs[:r % len(libs)]:
+            for _ in range(3):
+                assert l.ofs_sc_minn_metric(*args) == 0
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.steps):
+                l.ofs_sc_minn_metric(*args)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / a.steps)
+            if ref is None:
+                ref = [o.clone() for o in outs]
+            elif not a.no_check:
+                for o, q in zip(outs, ref):
+                    assert torch.equal(o, q), f"{name}: outputs differ"
+    alg = B * T * 8 * nb + 2 * B * nout * 16
+    for name, _ in libs:
+        ms = statistics.median(times[name])
+        print(json.dumps(dict(lib=name, op="scminn", shape=[B, nb, T, N], ms_median=round(ms, 4),
+                              ms_all=[round(t, 4) for t in times[name]], frac=round(alg / (ms / 1e3) / 8e12, 4))),
+              flush=True)
 
 
 if __name__ == "__main__":
