@@ -31,6 +31,9 @@ namespace {
 #endif
 constexpr int WF_WG = OFS_WF_WG;       // 4 waves = 4 streams per workgroup (tuning builds: 64)
 enum { WF_SC = 1, WF_COMB = 2, WF_MINN = 3 };
+typedef float wf4u __attribute__((ext_vector_type(4), aligned(8)));   // pair loads / stores at 8-byte alignment
+typedef float wf2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef float wf4ua __attribute__((ext_vector_type(4), aligned(4)));
 
 template <int MODE, int E, int MW, int NB>
 __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
@@ -73,15 +76,25 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
         for (int e = 0; e < E; ++e) { hR[m][e] = 0.f; hI[m][e] = 0.f; hE[m][e] = 0.f; }
 
     float4 nx[PD][NB][V4];
+    // whole rows: 8-byte-aligned float4 pair loads (any T: stream bases are float2-aligned);
+    // the last, partial row per sample with zeros past T (wave-uniform choice)
     auto load_row = [&](int k, float4 (&dst)[NB][V4]) {
+        const int64_t n0 = (int64_t)RL * k + E * lane;
+        const bool whole = (int64_t)RL * (k + 1) <= T;
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
-            const float4* xs = reinterpret_cast<const float4*>(xb + (int64_t)t * T);
+            const float2* xs = xb + (int64_t)t * T;
 #pragma unroll
             for (int j = 0; j < V4; ++j) {
-                int64_t q = ((int64_t)RL * k + E * lane) / 2 + j;   // float4 index (2 samples)
-                const int64_t qmax = T / 2 - 1;
-                dst[t][j] = xs[q < qmax ? q : qmax];                // zeroed on use past T
+                if (whole) {
+                    const wf4u v = *reinterpret_cast<const wf4u*>(xs + n0 + 2 * j);
+                    dst[t][j] = make_float4(v.x, v.y, v.z, v.w);
+                } else {
+                    const int64_t m0 = n0 + 2 * j;
+                    const float2 u0 = m0 < T ? xs[m0] : make_float2(0.f, 0.f);
+                    const float2 u1 = m0 + 1 < T ? xs[m0 + 1] : make_float2(0.f, 0.f);
+                    dst[t][j] = make_float4(u0.x, u0.y, u1.x, u1.y);
+                }
             }
         }
     };
@@ -103,11 +116,10 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
                 for (int t = 0; t < NB; ++t) {
                     float cr[E], ci[E];
 #pragma unroll
-                    for (int j = 0; j < V4; ++j) {
-                        const bool ok = nb + 2 * j < T;             // T even: pairs are whole
+                    for (int j = 0; j < V4; ++j) {                  // zeros past T from load_row
                         const float4 v = nx[u % PD][t][j];
-                        cr[2 * j] = ok ? v.x : 0.f; ci[2 * j] = ok ? v.y : 0.f;
-                        cr[2 * j + 1] = ok ? v.z : 0.f; ci[2 * j + 1] = ok ? v.w : 0.f;
+                        cr[2 * j] = v.x; ci[2 * j] = v.y;
+                        cr[2 * j + 1] = v.z; ci[2 * j + 1] = v.w;
                     }
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
@@ -171,21 +183,21 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
                 if (d0 >= 0 && d0 + E <= nout) {
 #pragma unroll
                     for (int j = 0; j < E; j += 4) {
-                        if constexpr (E >= 4) {
-                            if (a.M) *reinterpret_cast<float4*>(Mo + d0 + j) = make_float4(oM[j], oM[j + 1], oM[j + 2], oM[j + 3]);
-                            if (a.R) *reinterpret_cast<float4*>(Ro + d0 + j) = make_float4(oR[j], oR[j + 1], oR[j + 2], oR[j + 3]);
+                        if constexpr (E >= 4) {         // dword-aligned (gfx950 vector stores need only that)
+                            if (a.M) *reinterpret_cast<wf4ua*>(Mo + d0 + j) = wf4ua{oM[j], oM[j + 1], oM[j + 2], oM[j + 3]};
+                            if (a.R) *reinterpret_cast<wf4ua*>(Ro + d0 + j) = wf4ua{oR[j], oR[j + 1], oR[j + 2], oR[j + 3]};
                         }
                     }
                     if constexpr (E < 4) {
 #pragma unroll
                         for (int j = 0; j < E; j += 2) {
-                            if (a.M) *reinterpret_cast<float2*>(Mo + d0 + j) = make_float2(oM[j], oM[j + 1]);
-                            if (a.R) *reinterpret_cast<float2*>(Ro + d0 + j) = make_float2(oR[j], oR[j + 1]);
+                            if (a.M) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{oM[j], oM[j + 1]};
+                            if (a.R) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{oR[j], oR[j + 1]};
                         }
                     }
 #pragma unroll
                     for (int j = 0; j < E; j += 2)
-                        if (a.P) *reinterpret_cast<float4*>(Po + d0 + j) = make_float4(oPr[j], oPi[j], oPr[j + 1], oPi[j + 1]);
+                        if (a.P) *reinterpret_cast<wf4u*>(Po + d0 + j) = wf4u{oPr[j], oPi[j], oPr[j + 1], oPi[j + 1]};
                 } else {
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
@@ -222,9 +234,6 @@ struct WinFusedArgs {
 #ifndef OFS_SCM_ALIGN
 #define OFS_SCM_ALIGN 0
 #endif
-typedef float wf4u __attribute__((ext_vector_type(4), aligned(8)));
-typedef float wf2u __attribute__((ext_vector_type(2), aligned(4)));
-
 // occupancy bound (min waves per SIMD) of the fused kernel; tuning builds set -DOFS_SCM_WAVES=N
 #ifndef OFS_SCM_WAVES
 #define OFS_SCM_WAVES 0
@@ -492,7 +501,7 @@ int launch_fused(const WinFusedArgs& a, hipStream_t st) {
 }  // namespace
 
 int ofs_sc_minn_fast_plan(int fmt, int precision, int n_br, int64_t T, int N) {
-    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || (T & 1) || T < N || N % 4) return 0;
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || T < N || N % 4) return 0;
     const int Q = N / 4;
     for (int e : {4, 2}) {                     // per-wave LDS history: 64·E·(8·MW) floats
         if (Q % (64 * e)) continue;
@@ -526,7 +535,7 @@ int ofs_sc_minn_fast_try(int fmt, int precision, int n_br, const void* x, int64_
 }
 
 int ofs_win_fast_plan(int mode, int fmt, int precision, int n_br, int64_t T, int N) {
-    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || (T & 1) || T < N) return 0;
+    if (fmt != OFS_C64 || precision != OFS_FP32 || n_br < 1 || n_br > 2 || T < N) return 0;
     if (mode < WF_SC || mode > WF_MINN) return 0;
     const int div = mode == WF_MINN ? 4 : 2;
     if (N % div) return 0;

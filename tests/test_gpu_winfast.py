@@ -47,7 +47,7 @@ def relerr(a, b):
 
 @pytest.mark.parametrize("kind", ["sc", "comb", "minn"])
 @pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 1024), (1024, 3000), (512, 700), (256, 1024),
-                                 (4096, 6000), (2048, 2048)])
+                                 (4096, 6000), (2048, 2048), (1024, 3001), (512, 701), (2048, 4097)])
 def test_window_fast_path_vs_oracle(kind, N, T):
     plan = _lib.lib().ofs_win_plan(KIND[kind], _lib.C64, _lib.FP32, 1, T, N)
     # Minn N=256 (Q=64) is below the fast kernel's 128-sample row: general engine
@@ -75,7 +75,8 @@ def test_window_fast_path_covers_cfg4():
     assert L.ofs_win_plan(1, _lib.C128, _lib.FP64, 1, 4096, 2048) == 0     # fp64: general
 
 
-@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 1024), (512, 1500), (256, 800), (2048, 2100)])
+@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 1024), (512, 1500), (256, 800), (2048, 2100),
+                                 (2048, 4001), (512, 1501), (1024, 1025)])
 def test_fused_sc_minn_vs_oracle(N, T):
     """combined_sc_min's two metrics from the fused one-pass kernel (cfg4 shape first)."""
     plan = _lib.lib().ofs_win_plan(4, _lib.C64, _lib.FP32, 1, T, N)
@@ -106,7 +107,7 @@ def test_fused_sc_minn_general_fallback_fp64():
 
 
 @pytest.mark.parametrize("kind", ["sc", "comb", "minn", "fused"])
-@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 3000), (512, 900)])
+@pytest.mark.parametrize("N,T", [(2048, 4096), (1024, 3000), (512, 900), (1024, 3001)])
 def test_fast_paths_two_branches_vs_oracle(kind, N, T):
     """Two receive branches summed inside the streaming fast kernels (the reference's 2-D input,
     e.g. combined_sc_min.run_simulation on cir1[:2]): same tolerances as one branch."""

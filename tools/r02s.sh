@@ -1,0 +1,7 @@
+cd "${GRAFT_REPO_ROOT}"
+mkdir -p gpurun_out
+L=ofdm-sync-math_amd/ofdm_sync_amd/libofdmsync.so
+timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_winfast.py -m gpu > gpurun_out/r02s_tests.log 2>&1 || { echo "tests rc=$?"; exit 1; }
+timeout -k 10 200 python tools/lib_ab.py --op scminn --no-check --libs $L --B 32768 --T 4001 --L 512 --na 1 > gpurun_out/r02s_ab_odd.log 2>&1
+timeout -k 10 200 python tools/lib_ab.py --op scminn --no-check --libs $L --B 32768 --T 4096 --L 1024 --na 1 > gpurun_out/r02s_ab_cfg4.log 2>&1
+echo done
