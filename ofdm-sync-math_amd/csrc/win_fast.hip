@@ -214,6 +214,51 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     }
 }
 
+
+// Realigned row stores (OFS_SCM_ALIGN == 2): a lane owns 4 consecutive outputs at rowp + 4·lane,
+// which for 3 of 4 output rows [B][T-N+1] is not a 16-byte boundary.  Each lane instead stores the
+// aligned 16-byte chunk that ends inside its group, taking the leading o values from lane - 1
+// (DPP wave_shr:1); lane 0 stores its own leading 4 - o values and lane 63 its trailing o values
+// (the chunks straddling the neighbour rows).  o is wave-uniform.
+__device__ __forceinline__ float shr1f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+typedef float wf3u __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ void store_al4(float* rowp, const float (&v)[4], int lane) {
+    const int o = (int)(((uintptr_t)rowp >> 2) & 3);
+    float* p = rowp + 4 * lane;
+    const float p1 = shr1f(v[1]), p2 = shr1f(v[2]), p3 = shr1f(v[3]);
+    if (o == 0) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if (o == 1) {
+        if (lane) *reinterpret_cast<float4*>(p - 1) = make_float4(p3, v[0], v[1], v[2]);
+        else *reinterpret_cast<wf3u*>(p) = wf3u{v[0], v[1], v[2]};
+        if (lane == 63) p[3] = v[3];
+    } else if (o == 2) {
+        if (lane) *reinterpret_cast<float4*>(p - 2) = make_float4(p2, p3, v[0], v[1]);
+        else *reinterpret_cast<wf2u*>(p) = wf2u{v[0], v[1]};
+        if (lane == 63) *reinterpret_cast<wf2u*>(p + 2) = wf2u{v[2], v[3]};
+    } else {
+        if (lane) *reinterpret_cast<float4*>(p - 3) = make_float4(p1, p2, p3, v[0]);
+        else p[0] = v[0];
+        if (lane == 63) *reinterpret_cast<wf3u*>(p + 1) = wf3u{v[1], v[2], v[3]};
+    }
+}
+// complex outputs: 16 bytes = 2 values, so the group is 8-byte-shifted or aligned
+__device__ __forceinline__ void store_al2(float2* rowp, const float (&re)[4], const float (&im)[4], int lane) {
+    float2* p = rowp + 4 * lane;
+    const float qr = shr1f(re[3]), qi = shr1f(im[3]);
+    if ((((uintptr_t)rowp >> 3) & 1) == 0) {
+        *reinterpret_cast<float4*>(p) = make_float4(re[0], im[0], re[1], im[1]);
+        *reinterpret_cast<float4*>(p + 2) = make_float4(re[2], im[2], re[3], im[3]);
+    } else {
+        if (lane) *reinterpret_cast<float4*>(p - 1) = make_float4(qr, qi, re[0], im[0]);
+        else p[0] = make_float2(re[0], im[0]);
+        *reinterpret_cast<float4*>(p + 1) = make_float4(re[1], im[1], re[2], im[2]);
+        if (lane == 63) p[3] = make_float2(re[3], im[3]);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Fused combined_sc_min detector (cfg4): combined S&C (D = W = 2Q, R over both halves) AND
 // Minn (D = W = Q) from ONE pass over the stream, N = 4Q.  Lags in rows: Q = MW rows.
@@ -265,7 +310,7 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     // before the stream (zeros there) puts every full lane group of outputs on a 16-byte boundary
     // (flat SOL probe of this 1 : 4 read : write mix: 0.70 of peak with aligned 16-B stores
     // against 0.60 with misaligned 8-B ones).  Inputs then load 8-byte-aligned (f4u).
-    const int64_t s = OFS_SCM_ALIGN ? (((b * nout - (N - 1)) % 4) + 4) % 4 : 0;
+    const int64_t s = OFS_SCM_ALIGN == 1 ? (((b * nout - (N - 1)) % 4) + 4) % 4 : 0;
     const int nrows = (int)((T + s + RL - 1) / RL);
     const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
 
@@ -406,10 +451,24 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
                 const int64_t d0 = nb - (N - 1);
                 auto put = [&](float* Mo, float2* Po, float* Ro, const float (&m)[E], const float (&pr)[E],
                                const float (&pi)[E], const float (&r)[E]) {
-                    Mo += b * nout; Po += b * nout; Ro += b * nout;
+                    // null outputs stay null (offset only the requested ones)
+                    if (Mo) Mo += b * nout;
+                    if (Po) Po += b * nout;
+                    if (Ro) Ro += b * nout;
+#if OFS_SCM_ALIGN == 2
+                    if constexpr (E == 4) {                // whole row: 16-byte-aligned stores
+                        const int64_t r0 = (int64_t)RL * k - (N - 1);   // d of lane 0, element 0
+                        if (r0 >= 0 && r0 + RL <= nout) {               // wave-uniform
+                            if (Mo) store_al4(Mo + r0, m, lane);
+                            if (Ro) store_al4(Ro + r0, r, lane);
+                            if (Po) store_al2(Po + r0, pr, pi, lane);
+                            return;
+                        }
+                    }
+#endif
                     if (d0 >= 0 && d0 + E <= nout) {
                         if constexpr (E >= 4) {
-                            if (OFS_SCM_ALIGN) {                   // 16-byte aligned (row shift s)
+                            if (OFS_SCM_ALIGN == 1) {              // 16-byte aligned (row shift s)
 #pragma unroll
                                 for (int j = 0; j < E; j += 4) {
                                     if (Mo) *reinterpret_cast<float4*>(Mo + d0 + j) = make_float4(m[j], m[j + 1], m[j + 2], m[j + 3]);
@@ -446,6 +505,197 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
                 };
                 put(a.Ms, a.Ps, a.Rs, oMs, oPsr, oPsi, oRs);
                 put(a.Mm, a.Pm, a.Rm, oMm, oPmr, oPmi, oRm);
+            }
+        }
+    }
+}
+
+
+// Packed form of the fused kernel (OFS_SCM_PK, default): every complex quantity (the x ring, the
+// lag-2Q / lag-Q products, their in-lane partials, suffixes and window sums) is one 2 x fp32
+// register pair, so products, partials and window sums issue as v_pk_fma / v_pk_mul / v_pk_add
+// (half the VALU of the scalar form); the products are formed conjugated, conj(x[j])·x[j-D], so
+// P = Σ conj(a) needs no negation; both metrics share one packed multiply by rcp(R²) (1 ulp)
+// instead of two IEEE divisions.  Same cancellation-free window split and fp64 row scans.
+#ifndef OFS_SCM_PK
+#define OFS_SCM_PK 1
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
+// conj(c)·d = (c.x d.x + c.y d.y, c.x d.y - c.y d.x), accumulated into acc
+__device__ __forceinline__ pf2 cjmul_acc(pf2 c, pf2 d, pf2 acc) {
+    acc = __builtin_elementwise_fma(c.xx, d, acc);
+    return __builtin_elementwise_fma(c.yy, pf2{d.y, -d.x}, acc);
+}
+
+template <int E, int MW, int NB>
+__global__ OFS_SCM_BOUNDS void sc_minn_pk_kernel(WinFusedArgs a) {
+    constexpr int RL = 64 * E;
+    constexpr int N = 4 * MW * RL;
+    constexpr int XR = 2 * MW;                  // x ring / S_h suffix ring / S_q history ring
+    constexpr int ER = 4 * MW;                  // S_e history ring
+    constexpr int PD = 2;
+    constexpr int PER = ER;
+    constexpr int V4 = E / 2;
+    __shared__ float histE[WF_WG / 64][ER][E][64];     // S_e of the last ER rows
+    __shared__ pf2 histQ[WF_WG / 64][XR][E][64];       // conj S_q of the last XR rows
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)xcd_block_w() * (WF_WG / 64) + w;
+    if (b >= a.B) return;
+    const int64_t T = a.T;
+    const int64_t nout = T - N + 1;
+    const int nrows = (int)((T + RL - 1) / RL);
+    const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
+
+    pf2 xq[NB][XR][E];                          // x of rows k-2MW..k-1
+    pf2 shS[XR][E];                             // S_h suffixes (window 2Q = XR rows)
+    pf2 sqS[MW][E];                             // S_q suffixes (window Q = MW rows)
+    float seE[MW][E];                           // S_e suffixes
+    double chR[XR], chI[XR], cqR[MW], cqI[MW], ceE[MW];
+    double CHR = 0, CHI = 0, CQR = 0, CQI = 0, CEE = 0;
+#pragma unroll
+    for (int m = 0; m < XR; ++m) {
+        chR[m] = 0; chI[m] = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            shS[m][e] = pf2{0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < NB; ++t) xq[t][m][e] = pf2{0.f, 0.f};
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+        cqR[m] = 0; cqI[m] = 0; ceE[m] = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { sqS[m][e] = pf2{0.f, 0.f}; seE[m][e] = 0.f; }
+    }
+
+    float4 nx[PD][NB][V4];
+    // whole rows as 8-byte-aligned float4 pairs; the last, partial row per sample, zeros past T
+    auto load_row = [&](int k, float4 (&dst)[NB][V4]) {
+        const int64_t n0 = (int64_t)RL * k + E * lane;
+        const bool whole = (int64_t)RL * (k + 1) <= T;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            const float2* xs = xb + (int64_t)t * T;
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                if (whole) {
+                    const wf4u v = *reinterpret_cast<const wf4u*>(xs + n0 + 2 * j);
+                    dst[t][j] = make_float4(v.x, v.y, v.z, v.w);
+                } else {
+                    const int64_t m0 = n0 + 2 * j;
+                    const float2 u0 = m0 < T ? xs[m0] : make_float2(0.f, 0.f);
+                    const float2 u1 = m0 + 1 < T ? xs[m0 + 1] : make_float2(0.f, 0.f);
+                    dst[t][j] = make_float4(u0.x, u0.y, u1.x, u1.y);
+                }
+            }
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) load_row(p < nrows ? p : 0, nx[p]);
+
+    for (int k0 = 0; k0 < nrows; k0 += PER) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int k = k0 + u;
+            if (k < nrows) {
+                const int x2 = u % XR;                 // row k-2MW (x ring), then row k
+                const int x1 = (u + MW) % XR;          // row k-MW
+                pf2 h[E], q[E];
+                float en[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) { h[e] = pf2{0.f, 0.f}; q[e] = pf2{0.f, 0.f}; en[e] = 0.f; }
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {         // products summed over the branches
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const float4 v = nx[u % PD][t][e / 2];
+                        const pf2 c = (e & 1) ? pf2{v.z, v.w} : pf2{v.x, v.y};
+                        en[e] += fmaf(c.x, c.x, c.y * c.y);
+                        h[e] = cjmul_acc(c, xq[t][x2][e], h[e]);
+                        q[e] = cjmul_acc(c, xq[t][x1][e], q[e]);
+                        xq[t][x2][e] = c;
+                    }
+                }
+                if (k + PD < nrows) load_row(k + PD, nx[u % PD]);
+                // in-lane forward / backward partials, fp64 wave scans of the lane totals
+                pf2 fh[E], gh[E], fq[E], gq[E];
+                float fe[E], ge[E];
+                fh[0] = h[0]; fq[0] = q[0]; fe[0] = en[0];
+#pragma unroll
+                for (int e = 1; e < E; ++e) { fh[e] = fh[e - 1] + h[e]; fq[e] = fq[e - 1] + q[e]; fe[e] = fe[e - 1] + en[e]; }
+                gh[E - 1] = pf2{0.f, 0.f}; gq[E - 1] = pf2{0.f, 0.f}; ge[E - 1] = 0.f;
+#pragma unroll
+                for (int e = E - 2; e >= 0; --e) { gh[e] = gh[e + 1] + h[e + 1]; gq[e] = gq[e + 1] + q[e + 1]; ge[e] = ge[e + 1] + en[e + 1]; }
+                const double ihR = scan_add((double)fh[E - 1].x), ihI = scan_add((double)fh[E - 1].y);
+                const double iqR = scan_add((double)fq[E - 1].x), iqI = scan_add((double)fq[E - 1].y);
+                const double ie = scan_add((double)fe[E - 1]);
+                const double thR = readlane(ihR, 63), thI = readlane(ihI, 63);
+                const double tqR = readlane(iqR, 63), tqI = readlane(iqI, 63), te = readlane(ie, 63);
+                const pf2 xh = pf2{(float)shr1z(ihR), (float)shr1z(ihI)}, uh = pf2{(float)(thR - ihR), (float)(thI - ihI)};
+                const pf2 xqq = pf2{(float)shr1z(iqR), (float)shr1z(iqI)}, uq = pf2{(float)(tqR - iqR), (float)(tqI - iqI)};
+                const float xe = (float)shr1z(ie), ue = (float)(te - ie);
+                const int sq = u % MW, soq = (u + 1) % MW, soh = (u + 1) % XR;
+                const pf2 wh = k >= XR ? pf2{(float)(CHR - chR[soh]), (float)(CHI - chI[soh])} : pf2{(float)CHR, (float)CHI};
+                const pf2 wq = k >= MW ? pf2{(float)(CQR - cqR[soq]), (float)(CQI - cqI[soq])} : pf2{(float)CQR, (float)CQI};
+                const float we = (float)(k >= MW ? CEE - ceE[soq] : CEE);
+                const int e0 = u % ER, e1 = (u + 3 * MW) % ER, e2 = (u + 2 * MW) % ER, e3 = (u + MW) % ER;
+                float oMs[E], oRs[E], oMm[E], oRm[E];
+                pf2 oPs[E], oPm[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    pf2 SH = wh + (xh + fh[e]), SQ = wq + (xqq + fq[e]);
+                    float SE = we + (xe + fe[e]);
+                    if (k >= XR) SH += shS[x2][e];
+                    if (k >= MW) { SQ += sqS[sq][e]; SE += seE[sq][e]; }
+                    shS[x2][e] = uh + gh[e];
+                    sqS[sq][e] = uq + gq[e];
+                    seE[sq][e] = ue + ge[e];
+                    // histories (LDS): S_e rows k-MW, k-2MW, k-3MW; S_q row k-2MW
+                    const float E1 = histE[w][e1][e][lane], E2 = histE[w][e2][e][lane], E3 = histE[w][e3][e][lane];
+                    const pf2 Q2 = histQ[w][x2][e][lane];
+                    histE[w][e0][e][lane] = SE;
+                    histQ[w][x2][e][lane] = SQ;
+                    const float Rm = SE + E1 + E2;
+                    const float Rs = Rm + E3;
+                    const pf2 Pm = SQ + Q2;
+                    const float ds = fmaxf(Rs, 1e-12f), dm = fmaxf(Rm, 1e-12f);
+                    const pf2 d2 = pf2{ds, dm} * pf2{ds, dm};
+                    const float pmr = fmaxf(Pm.x, 0.f);
+                    const pf2 num = pf2{fmaf(SH.x, SH.x, SH.y * SH.y), pmr * pmr};
+                    const pf2 mm = num * pf2{__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y)};
+                    oMs[e] = mm.x; oMm[e] = mm.y; oRs[e] = Rs; oRm[e] = Rm; oPs[e] = SH; oPm[e] = Pm;
+                }
+                chR[soh] = CHR + thR; chI[soh] = CHI + thI;
+                cqR[soq] = CQR + tqR; cqI[soq] = CQI + tqI; ceE[soq] = CEE + te;
+                CHR += thR; CHI += thI; CQR += tqR; CQI += tqI; CEE += te;
+                const int64_t d0 = (int64_t)RL * k + E * lane - (N - 1);
+                auto put = [&](float* Mo, float2* Po, float* Ro, const float (&m)[E], const pf2 (&pp)[E], const float (&r)[E]) {
+                    if (Mo) Mo += b * nout;
+                    if (Po) Po += b * nout;
+                    if (Ro) Ro += b * nout;
+                    if (d0 >= 0 && d0 + E <= nout) {
+#pragma unroll
+                        for (int j = 0; j < E; j += 2) {
+                            if (Mo) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{m[j], m[j + 1]};
+                            if (Ro) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{r[j], r[j + 1]};
+                            if (Po) *reinterpret_cast<wf4u*>(Po + d0 + j) = wf4u{pp[j].x, pp[j].y, pp[j + 1].x, pp[j + 1].y};
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int64_t d = d0 + e;
+                            if (d >= 0 && d < nout) {
+                                if (Mo) Mo[d] = m[e];
+                                if (Po) Po[d] = make_float2(pp[e].x, pp[e].y);
+                                if (Ro) Ro[d] = r[e];
+                            }
+                        }
+                    }
+                };
+                put(a.Ms, a.Ps, a.Rs, oMs, oPs, oRs);
+                put(a.Mm, a.Pm, a.Rm, oMm, oPm, oRm);
             }
         }
     }
@@ -494,7 +744,10 @@ void pick(int W, int& E, int& mw) {
 template <int E, int MW, int NB>
 int launch_fused(const WinFusedArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
-    hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    if (OFS_SCM_PK)
+        hipLaunchKernelGGL((sc_minn_pk_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    else
+        hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
