@@ -35,6 +35,14 @@ typedef float wf4u __attribute__((ext_vector_type(4), aligned(8)));   // pair lo
 typedef float wf2u __attribute__((ext_vector_type(2), aligned(4)));
 typedef float wf4ua __attribute__((ext_vector_type(4), aligned(4)));
 
+// packed fp32 pairs (re, im): products, partials and window sums issue as v_pk_* (see the fused
+// kernel below); conj(c)·d accumulated, so P = Σ conj(a) needs no negation
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 cjmul_acc(pf2 c, pf2 d, pf2 acc) {
+    acc = __builtin_elementwise_fma(c.xx, d, acc);
+    return __builtin_elementwise_fma(c.yy, pf2{d.y, -d.x}, acc);
+}
+
 template <int MODE, int E, int MW, int NB>
 __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     constexpr int RL = 64 * E;
@@ -51,13 +59,15 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
     const int64_t nout = T - N + 1;
     const int nrows = (int)((T + RL - 1) / RL);
     const float2* xb = reinterpret_cast<const float2*>(a.x) + b * NB * T;   // [NB][T] of stream b
-    float* Mo = reinterpret_cast<float*>(a.M) + b * nout;
-    float2* Po = reinterpret_cast<float2*>(a.P) + b * nout;
-    float* Ro = reinterpret_cast<float*>(a.R) + b * nout;
+    float* Mo = a.M ? reinterpret_cast<float*>(a.M) + b * nout : nullptr;
+    float2* Po = a.P ? reinterpret_cast<float2*>(a.P) + b * nout : nullptr;
+    float* Ro = a.R ? reinterpret_cast<float*>(a.R) + b * nout : nullptr;
 
-    float lr[NB][MW][E], li[NB][MW][E];          // x of rows k-MW..k-1 (lag D = W), per branch
-    float sR[MW][E], sI[MW][E], sE[MW][E];       // retained in-window suffixes
-    float hR[HR][E], hI[HR][E], hE[HR][E];       // window sums of past rows (COMB/MINN)
+    pf2 lx[NB][MW][E];                           // x of rows k-MW..k-1 (lag D = W), per branch
+    pf2 sS[MW][E];                               // retained in-window suffixes (conj products)
+    float sE[MW][E];
+    pf2 hS[HR][E];                               // window sums of past rows (MINN: products)
+    float hE[HR][E];                             // (COMB / MINN: energies)
     double cbR[MW], cbI[MW], cbE[MW];            // row bases C[j] for j in (k-MW, k]
     double CR = 0.0, CI = 0.0, CE = 0.0;         // C[k]: prefix at the start of row k
 #pragma unroll
@@ -65,15 +75,15 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
         cbR[m] = 0.0; cbI[m] = 0.0; cbE[m] = 0.0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            sR[m][e] = 0.f; sI[m][e] = 0.f; sE[m][e] = 0.f;
+            sS[m][e] = pf2{0.f, 0.f}; sE[m][e] = 0.f;
 #pragma unroll
-            for (int t = 0; t < NB; ++t) { lr[t][m][e] = 0.f; li[t][m][e] = 0.f; }
+            for (int t = 0; t < NB; ++t) lx[t][m][e] = pf2{0.f, 0.f};
         }
     }
 #pragma unroll
     for (int m = 0; m < HR; ++m)
 #pragma unroll
-        for (int e = 0; e < E; ++e) { hR[m][e] = 0.f; hI[m][e] = 0.f; hE[m][e] = 0.f; }
+        for (int e = 0; e < E; ++e) { hS[m][e] = pf2{0.f, 0.f}; hE[m][e] = 0.f; }
 
     float4 nx[PD][NB][V4];
     // whole rows: 8-byte-aligned float4 pair loads (any T: stream bases are float2-aligned);
@@ -106,72 +116,66 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
         for (int u = 0; u < PER; ++u) {
             const int k = k0 + u;
             if (k < nrows) {
-                const int64_t nb = (int64_t)RL * k + E * lane;
                 const int sl = u % MW;                              // ring slot of row k (and k-MW)
-                // ---- lagged products and energies (fp32), summed over the branches ----
-                float aR[E], aI[E], aE[E];
+                // ---- lagged products conj(x[j])·x[j-D] and energies, summed over the branches ----
+                pf2 av[E];
+                float aE[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+                for (int e = 0; e < E; ++e) { av[e] = pf2{0.f, 0.f}; aE[e] = 0.f; }
 #pragma unroll
                 for (int t = 0; t < NB; ++t) {
-                    float cr[E], ci[E];
 #pragma unroll
-                    for (int j = 0; j < V4; ++j) {                  // zeros past T from load_row
-                        const float4 v = nx[u % PD][t][j];
-                        cr[2 * j] = v.x; ci[2 * j] = v.y;
-                        cr[2 * j + 1] = v.z; ci[2 * j + 1] = v.w;
-                    }
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        aE[e] += fmaf(cr[e], cr[e], ci[e] * ci[e]);
-                        if (k >= MW) {
-                            aR[e] += fmaf(cr[e], lr[t][sl][e], ci[e] * li[t][sl][e]);
-                            aI[e] += fmaf(ci[e], lr[t][sl][e], -(cr[e] * li[t][sl][e]));
-                        }
-                        lr[t][sl][e] = cr[e]; li[t][sl][e] = ci[e];
+                    for (int e = 0; e < E; ++e) {                   // zeros past T from load_row
+                        const float4 v = nx[u % PD][t][e / 2];
+                        const pf2 c = (e & 1) ? pf2{v.z, v.w} : pf2{v.x, v.y};
+                        aE[e] += fmaf(c.x, c.x, c.y * c.y);
+                        if (k >= MW) av[e] = cjmul_acc(c, lx[t][sl][e], av[e]);
+                        lx[t][sl][e] = c;
                     }
                 }
                 if (k + PD < nrows) load_row(k + PD, nx[u % PD]);   // PD rows ahead
                 // ---- in-lane partials (forward f, backward g) ----
-                float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
-                fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+                pf2 fS[E], gS[E];
+                float fE[E], gE[E];
+                fS[0] = av[0]; fE[0] = aE[0];
 #pragma unroll
-                for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
-                gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+                for (int e = 1; e < E; ++e) { fS[e] = fS[e - 1] + av[e]; fE[e] = fE[e - 1] + aE[e]; }
+                gS[E - 1] = pf2{0.f, 0.f}; gE[E - 1] = 0.f;
 #pragma unroll
-                for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+                for (int e = E - 2; e >= 0; --e) { gS[e] = gS[e + 1] + av[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
                 // ---- lane totals: fp64 wave scan; row totals; rows strictly inside the window ----
-                const double iR = scan_add((double)fR[E - 1]), iI = scan_add((double)fI[E - 1]), iE = scan_add((double)fE[E - 1]);
+                const double iR = scan_add((double)fS[E - 1].x), iI = scan_add((double)fS[E - 1].y), iE = scan_add((double)fE[E - 1]);
                 const double tR = readlane(iR, 63), tI = readlane(iI, 63), tE = readlane(iE, 63);
-                const float xR = (float)shr1z(iR), xI = (float)shr1z(iI), xE = (float)shr1z(iE);
-                const float uR = (float)(tR - iR), uI = (float)(tI - iI), uE = (float)(tE - iE);
+                const pf2 xS = pf2{(float)shr1z(iR), (float)shr1z(iI)}, uS = pf2{(float)(tR - iR), (float)(tI - iI)};
+                const float xE = (float)shr1z(iE), uE = (float)(tE - iE);
                 const int so = (u + 1) % MW;                        // slot of C[k-MW+1]
-                const float wR = (float)(k >= MW ? CR - cbR[so] : CR);
-                const float wI = (float)(k >= MW ? CI - cbI[so] : CI);
+                const pf2 wS = k >= MW ? pf2{(float)(CR - cbR[so]), (float)(CI - cbI[so])} : pf2{(float)CR, (float)CI};
                 const float wE = (float)(k >= MW ? CE - cbE[so] : CE);
                 // ---- window sums, outputs ----
-                float oM[E], oPr[E], oPi[E], oR[E];
+                float oM[E], oR[E];
+                pf2 oP[E];
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    float SR = wR + (xR + fR[e]), SI = wI + (xI + fI[e]), SE = wE + (xE + fE[e]);
-                    if (k >= MW) { SR += sR[sl][e]; SI += sI[sl][e]; SE += sE[sl][e]; }
-                    sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
-                    float PR = SR, PI = SI, RR = SE;
+                    pf2 S = wS + (xS + fS[e]);
+                    float SE = wE + (xE + fE[e]);
+                    if (k >= MW) { S += sS[sl][e]; SE += sE[sl][e]; }
+                    sS[sl][e] = uS + gS[e]; sE[sl][e] = uE + gE[e];
+                    pf2 P = S;
+                    float RR = SE;
                     if constexpr (MODE == WF_COMB) {
                         RR += hE[sl][e];                            // S_e(n - W): row k-MW
                         hE[sl][e] = SE;
                     } else if constexpr (MODE == WF_MINN) {
                         const int h2 = u % HR;                      // row k-2MW (and k)
                         const int h1 = (u + MW) % HR;               // row k-MW
-                        PR += hR[h2][e]; PI += hI[h2][e];
+                        P += hS[h2][e];
                         RR += hE[h1][e] + hE[h2][e];
-                        hR[h2][e] = SR; hI[h2][e] = SI; hE[h2][e] = SE;
+                        hS[h2][e] = S; hE[h2][e] = SE;
                     }
-                    PI = -PI;                                       // P = conj(window sum)
                     const float den = fmaxf(RR, 1e-12f);
-                    const float num = (MODE == WF_MINN) ? fmaxf(PR, 0.f) * fmaxf(PR, 0.f) : fmaf(PR, PR, PI * PI);
-                    oM[e] = num / (den * den);
-                    oPr[e] = PR; oPi[e] = PI; oR[e] = RR;
+                    const float num = (MODE == WF_MINN) ? fmaxf(P.x, 0.f) * fmaxf(P.x, 0.f) : fmaf(P.x, P.x, P.y * P.y);
+                    oM[e] = num * __builtin_amdgcn_rcpf(den * den);
+                    oP[e] = P; oR[e] = RR;
                 }
                 // C[k+1] replaces C[k-MW+1] in the ring
                 cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
@@ -179,33 +183,32 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
                 // ---- stores: outputs d = n - (N-1) in [0, nout) ----
                 // a lane's E outputs are contiguous: dword-aligned vector stores (the output
                 // rows [B][T-N+1] are not 16-byte aligned; gfx950 global stores allow it)
-                const int64_t d0 = nb - (N - 1);
+                const int64_t d0 = (int64_t)RL * k + E * lane - (N - 1);
                 if (d0 >= 0 && d0 + E <= nout) {
+                    if constexpr (E >= 4) {
 #pragma unroll
-                    for (int j = 0; j < E; j += 4) {
-                        if constexpr (E >= 4) {         // dword-aligned (gfx950 vector stores need only that)
-                            if (a.M) *reinterpret_cast<wf4ua*>(Mo + d0 + j) = wf4ua{oM[j], oM[j + 1], oM[j + 2], oM[j + 3]};
-                            if (a.R) *reinterpret_cast<wf4ua*>(Ro + d0 + j) = wf4ua{oR[j], oR[j + 1], oR[j + 2], oR[j + 3]};
+                        for (int j = 0; j < E; j += 4) {
+                            if (Mo) *reinterpret_cast<wf4ua*>(Mo + d0 + j) = wf4ua{oM[j], oM[j + 1], oM[j + 2], oM[j + 3]};
+                            if (Ro) *reinterpret_cast<wf4ua*>(Ro + d0 + j) = wf4ua{oR[j], oR[j + 1], oR[j + 2], oR[j + 3]};
                         }
-                    }
-                    if constexpr (E < 4) {
+                    } else {
 #pragma unroll
                         for (int j = 0; j < E; j += 2) {
-                            if (a.M) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{oM[j], oM[j + 1]};
-                            if (a.R) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{oR[j], oR[j + 1]};
+                            if (Mo) *reinterpret_cast<wf2u*>(Mo + d0 + j) = wf2u{oM[j], oM[j + 1]};
+                            if (Ro) *reinterpret_cast<wf2u*>(Ro + d0 + j) = wf2u{oR[j], oR[j + 1]};
                         }
                     }
 #pragma unroll
                     for (int j = 0; j < E; j += 2)
-                        if (a.P) *reinterpret_cast<wf4u*>(Po + d0 + j) = wf4u{oPr[j], oPi[j], oPr[j + 1], oPi[j + 1]};
+                        if (Po) *reinterpret_cast<wf4u*>(Po + d0 + j) = wf4u{oP[j].x, oP[j].y, oP[j + 1].x, oP[j + 1].y};
                 } else {
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
                         const int64_t d = d0 + e;
                         if (d >= 0 && d < nout) {
-                            if (a.M) Mo[d] = oM[e];
-                            if (a.P) Po[d] = make_float2(oPr[e], oPi[e]);
-                            if (a.R) Ro[d] = oR[e];
+                            if (Mo) Mo[d] = oM[e];
+                            if (Po) Po[d] = make_float2(oP[e].x, oP[e].y);
+                            if (Ro) Ro[d] = oR[e];
                         }
                     }
                 }
@@ -213,7 +216,6 @@ __global__ __launch_bounds__(WF_WG) void win_fast_kernel(WinFastArgs a) {
         }
     }
 }
-
 
 // Realigned row stores (OFS_SCM_ALIGN == 2): a lane owns 4 consecutive outputs at rowp + 4·lane,
 // which for 3 of 4 output rows [B][T-N+1] is not a 16-byte boundary.  Each lane instead stores the
@@ -520,12 +522,6 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
 #ifndef OFS_SCM_PK
 #define OFS_SCM_PK 1
 #endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
-// conj(c)·d = (c.x d.x + c.y d.y, c.x d.y - c.y d.x), accumulated into acc
-__device__ __forceinline__ pf2 cjmul_acc(pf2 c, pf2 d, pf2 acc) {
-    acc = __builtin_elementwise_fma(c.xx, d, acc);
-    return __builtin_elementwise_fma(c.yy, pf2{d.y, -d.x}, acc);
-}
 
 template <int E, int MW, int NB>
 __global__ OFS_SCM_BOUNDS void sc_minn_pk_kernel(WinFusedArgs a) {

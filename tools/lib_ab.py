@@ -31,10 +31,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--detect-only", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="variants may differ in rounding (no bit-equality check)")
-    ap.add_argument("--op", choices=("aa", "scminn"), default="aa", help="aa: ofs_aa_detect; scminn: "
+    ap.add_argument("--op", choices=("aa", "scminn", "sc", "comb", "minn"), default="aa", help="aa: ofs_aa_detect; scminn: "
                     "ofs_sc_minn_metric (cfg4 fused S&C + Minn, N = 2 L)")
     a = ap.parse_args()
-    if a.op == "scminn":
+    if a.op != "aa":
         return scminn(a)
     dev = torch.device("cuda", 0)
     B, T, L, na, E = a.B, a.T, a.L, a.na, 4
@@ -88,14 +88,22 @@ def scminn(a):
     B, T, N, nb = a.B, a.T, 2 * a.L, a.na
     x = synth.synth_batch(synth.faded_base(a.L, "cir1", tuple(range(nb)) if nb > 1 else (1,)), B, T, seed=4, device=dev)
     nout = T - N + 1
-    outs = [torch.empty((B, nout), dtype=dt, device=dev) for dt in (torch.float32, torch.complex64, torch.float32) * 2]
+    n_sets = 2 if a.op == "scminn" else 1
+    outs = [torch.empty((B, nout), dtype=dt, device=dev) for dt in (torch.float32, torch.complex64, torch.float32) * n_sets]
     st = torch.cuda.current_stream(dev)
     libs = []
     for p in a.libs.split(","):
         l = ctypes.CDLL(os.path.abspath(p))
         _lib._declare(l)
         libs.append((os.path.basename(p), l))
-    args = (_lib.C64, x.data_ptr(), B, nb, T, N, _lib.FP32, *[o.data_ptr() for o in outs], st.cuda_stream)
+    optr = [o.data_ptr() for o in outs]
+    if a.op == "scminn":
+        call = lambda l: l.ofs_sc_minn_metric(_lib.C64, x.data_ptr(), B, nb, T, N, _lib.FP32, *optr, st.cuda_stream)
+    elif a.op == "minn":
+        call = lambda l: l.ofs_minn_metric(_lib.C64, x.data_ptr(), B, nb, T, N, _lib.FP32, *optr, st.cuda_stream)
+    else:
+        rm = 0 if a.op == "sc" else 1
+        call = lambda l: l.ofs_sc_metric(_lib.C64, x.data_ptr(), B, nb, T, N, rm, _lib.FP32, *optr, st.cuda_stream)
     times = {n: [] for n, _ in libs}
     ref = None
     for r in range(a.rounds):
@@ -104,12 +112,12 @@ def scminn(a):
                 for o in outs:
                     o.fill_(float("nan"))
             for _ in range(3):
-                assert l.ofs_sc_minn_metric(*args) == 0
+                assert call(l) == 0
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(a.steps):
-                l.ofs_sc_minn_metric(*args)
+                call(l)
             e1.record(st)
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / a.steps)
@@ -118,10 +126,10 @@ def scminn(a):
             elif not a.no_check:
                 for o, q in zip(outs, ref):
                     assert torch.equal(o, q), f"{name}: outputs differ"
-    alg = B * T * 8 * nb + 2 * B * nout * 16
+    alg = B * T * 8 * nb + n_sets * B * nout * 16
     for name, _ in libs:
         ms = statistics.median(times[name])
-        print(json.dumps(dict(lib=name, op="scminn", shape=[B, nb, T, N], ms_median=round(ms, 4),
+        print(json.dumps(dict(lib=name, op=a.op, shape=[B, nb, T, N], ms_median=round(ms, 4),
                               ms_all=[round(t, 4) for t in times[name]], frac=round(alg / (ms / 1e3) / 8e12, 4))),
               flush=True)
 
