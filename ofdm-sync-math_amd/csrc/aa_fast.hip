@@ -55,6 +55,14 @@ constexpr int TMAX = 1024;        // stream length handled by the fast path
 #endif
 typedef float nf4 __attribute__((ext_vector_type(4)));
 typedef float nf2 __attribute__((ext_vector_type(2)));
+// complex values as packed fp32 pairs (re, im): products, in-lane partials and window sums issue
+// as v_pk_fma / v_pk_add (half the VALU of the scalar form)
+typedef float pf2 __attribute__((ext_vector_type(2)));
+// acc + c·conj(d) = acc + (c.x d.x + c.y d.y, c.y d.x - c.x d.y)
+__device__ __forceinline__ pf2 mulc_acc(pf2 c, pf2 d, pf2 acc) {
+    acc = __builtin_elementwise_fma(c, d.xx, acc);
+    return __builtin_elementwise_fma(c.yx, pf2{d.y, -d.y}, acc);
+}
 __device__ __forceinline__ void st_out(float4* p, float4 v) {
 #if OFS_STORE_NT
     __builtin_nontemporal_store(nf4{v.x, v.y, v.z, v.w}, reinterpret_cast<nf4*>(p));
@@ -127,17 +135,18 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     }
     auto ldrow = [&](int t, int k, int j) { return xreg[t][k][j]; };
 #endif
-    auto xrow = [&](int t, int k, float (&re)[E], float (&im)[E]) {
+    auto xrow = [&](int t, int k, pf2 (&c)[E]) {
 #pragma unroll
         for (int j = 0; j < V4; ++j) {
             const bool ok = RL * k + E * lane + 2 * j < T;
             const float4 v = ldrow(t, k, j);
-            re[2 * j] = ok ? v.x : 0.f; im[2 * j] = ok ? v.y : 0.f;
-            re[2 * j + 1] = ok ? v.z : 0.f; im[2 * j + 1] = ok ? v.w : 0.f;
+            c[2 * j] = ok ? pf2{v.x, v.y} : pf2{0.f, 0.f};
+            c[2 * j + 1] = ok ? pf2{v.z, v.w} : pf2{0.f, 0.f};
         }
     };
 
-    float sR[MR][E], sI[MR][E], sE[MR][E];      // retained in-window suffixes (ring by k % MR)
+    pf2 sS[MR][E];                              // retained in-window suffixes (ring by k % MR)
+    float sE[MR][E];
     double Cr[RW + 1], Ci[RW + 1], Ce[RW + 1];  // running row bases (wave-uniform)
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
@@ -158,57 +167,57 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
             // ---- lagged products x[n]·conj(x[n-L]) and energies, fp32 ----
             // summed over the antennas, like the reference's per-antenna running sums added up
             // (sync_aa.py:463-480)
-            float aR[E], aI[E], aE[E];
+            pf2 av[E];
+            float aE[E];
 #pragma unroll
-            for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+            for (int e = 0; e < E; ++e) { av[e] = pf2{0.f, 0.f}; aE[e] = 0.f; }
 #pragma unroll
             for (int t = 0; t < NA; ++t) {
-                float cr[E], ci[E];
-                xrow(t, k, cr, ci);
+                pf2 c[E];
+                xrow(t, k, c);
 #pragma unroll
-                for (int e = 0; e < E; ++e) aE[e] += fmaf(cr[e], cr[e], ci[e] * ci[e]);
+                for (int e = 0; e < E; ++e) aE[e] += fmaf(c[e].x, c[e].x, c[e].y * c[e].y);
                 if (k >= MR) {
-                    float dr[E], di[E];
-                    xrow(t, k - MR, dr, di);
+                    pf2 d[E];
+                    xrow(t, k - MR, d);
 #pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        aR[e] += fmaf(cr[e], dr[e], ci[e] * di[e]);
-                        aI[e] += fmaf(ci[e], dr[e], -(cr[e] * di[e]));
-                    }
+                    for (int e = 0; e < E; ++e) av[e] = mulc_acc(c[e], d[e], av[e]);
                 }
             }
             // ---- in-lane partials, each summing only the terms it stands for:
             //      forward f[e] = sum_{e'<=e} a[e'], backward g[e] = sum_{e'>e} a[e'] ----
-            float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
-            fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+            pf2 fS[E], gS[E];
+            float fE[E], gE[E];
+            fS[0] = av[0]; fE[0] = aE[0];
 #pragma unroll
-            for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
-            gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+            for (int e = 1; e < E; ++e) { fS[e] = fS[e - 1] + av[e]; fE[e] = fE[e - 1] + aE[e]; }
+            gS[E - 1] = pf2{0.f, 0.f}; gE[E - 1] = 0.f;
 #pragma unroll
-            for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+            for (int e = E - 2; e >= 0; --e) { gS[e] = gS[e + 1] + av[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
             // ---- lane totals: fp64 DPP wave scan, row totals, rows inside the window ----
-            const RowScan sRr = row_scan(fR[E - 1]), sIr = row_scan(fI[E - 1]), sEr = row_scan(fE[E - 1]);
+            const RowScan sRr = row_scan(fS[E - 1].x), sIr = row_scan(fS[E - 1].y), sEr = row_scan(fE[E - 1]);
             const double totR = sRr.tot, totI = sIr.tot, totE = sEr.tot;
-            const float xR = sRr.x, xI = sIr.x, xE = sEr.x;             // lanes < l
-            const float uR = sRr.u, uI = sIr.u, uE = sEr.u;             // lanes > l
+            const pf2 xS = pf2{sRr.x, sIr.x};                        // lanes < l
+            const float xE = sEr.x;
+            const pf2 uS = pf2{sRr.u, sIr.u};                        // lanes > l
+            const float uE = sEr.u;
             Cr[k + 1] = Cr[k] + totR; Ci[k + 1] = Ci[k] + totI; Ce[k + 1] = Ce[k] + totE;
-            const float wR = (float)((k >= MR) ? (Cr[k] - Cr[k - MR + 1]) : Cr[k]);
-            const float wI = (float)((k >= MR) ? (Ci[k] - Ci[k - MR + 1]) : Ci[k]);
+            const pf2 wS = pf2{(float)((k >= MR) ? (Cr[k] - Cr[k - MR + 1]) : Cr[k]),
+                               (float)((k >= MR) ? (Ci[k] - Ci[k - MR + 1]) : Ci[k])};
             const float wE = (float)((k >= MR) ? (Ce[k] - Ce[k - MR + 1]) : Ce[k]);
 
             // ---- window sums  P = suffix(row k-MR) + rows between + prefix(row k) ----
             float pf[E][2], mf[E], pmf[E], rf[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                float PR = wR + (xR + fR[e]);
-                float PI = wI + (xI + fI[e]);
+                pf2 P = wS + (xS + fS[e]);
                 float RR = wE + (xE + fE[e]);
-                if (k >= MR) { PR += sR[k % MR][e]; PI += sI[k % MR][e]; RR += sE[k % MR][e]; }
-                sR[k % MR][e] = uR + gR[e]; sI[k % MR][e] = uI + gI[e]; sE[k % MR][e] = uE + gE[e];
-                const float pm = fmaf(PR, PR, PI * PI);
+                if (k >= MR) { P += sS[k % MR][e]; RR += sE[k % MR][e]; }
+                sS[k % MR][e] = uS + gS[e]; sE[k % MR][e] = uE + gE[e];
+                const float pm = fmaf(P.x, P.x, P.y * P.y);
                 float m = 0.f;
                 if (k >= MR && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
-                pf[e][0] = PR; pf[e][1] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
+                pf[e][0] = P.x; pf[e][1] = P.y; rf[e] = RR; mf[e] = m; pmf[e] = pm;
             }
 
             const int64_t o = b * a.T + nb;
@@ -305,8 +314,9 @@ struct AaStream {
     float4 (*lag)[NA][V4][64];                               // LDSLAG: [MR][NA][V4][lane]
     int64_t T, o0;
     int Ti, nrows, full_rows, lane;
-    float lr[LDSLAG ? 1 : NA][MR][E], li[LDSLAG ? 1 : NA][MR][E];   // x of rows k-MR..k-1 (lag L)
-    float sR[MR][E], sI[MR][E], sE[MR][E];                   // retained in-window suffixes
+    pf2 lx[LDSLAG ? 1 : NA][MR][E];                          // x of rows k-MR..k-1 (lag L)
+    pf2 sS[MR][E];                                           // retained in-window suffixes
+    float sE[MR][E];
     double cbR[MR], cbI[MR], cbE[MR];                        // row bases C[j], j in (k-MR, k]
     double CR, CI, CE;                                       // C[k]: prefix at the start of row k
     float2 nx[PD][NA][E];                                    // rows k..k+PD-1 in flight
@@ -348,73 +358,72 @@ struct AaStream {
             for (int e = 0; e < E; ++e) cur[t][e] = nx[U % PD][t][e];
         if (!GUARD || k + PD < nrows) load_row(k + PD, nx[U % PD]);
         // lagged samples x[n-L] (row k-MR) of every antenna
-        float dr[NA][E], di[NA][E];
+        pf2 d[NA][E];
 #pragma unroll
         for (int t = 0; t < NA; ++t) {
             if constexpr (LDSLAG) {
 #pragma unroll
                 for (int j = 0; j < V4; ++j) {
                     const float4 v = FIRST ? make_float4(0.f, 0.f, 0.f, 0.f) : lag[sl][t][j][lane];
-                    dr[t][2 * j] = v.x; di[t][2 * j] = v.y; dr[t][2 * j + 1] = v.z; di[t][2 * j + 1] = v.w;
+                    d[t][2 * j] = pf2{v.x, v.y}; d[t][2 * j + 1] = pf2{v.z, v.w};
                     lag[sl][t][j][lane] = make_float4(cur[t][2 * j].x, cur[t][2 * j].y, cur[t][2 * j + 1].x,
                                                       cur[t][2 * j + 1].y);
                 }
             } else {
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    dr[t][e] = lr[t][sl][e]; di[t][e] = li[t][sl][e];
-                    lr[t][sl][e] = cur[t][e].x; li[t][sl][e] = cur[t][e].y;
+                    d[t][e] = lx[t][sl][e];
+                    lx[t][sl][e] = pf2{cur[t][e].x, cur[t][e].y};
                 }
             }
         }
         // ---- lagged products x[n]·conj(x[n-L]) and energies, summed over the antennas ----
-        float aR[E], aI[E], aE[E];
+        pf2 av[E];
+        float aE[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) { aR[e] = 0.f; aI[e] = 0.f; aE[e] = 0.f; }
+        for (int e = 0; e < E; ++e) { av[e] = pf2{0.f, 0.f}; aE[e] = 0.f; }
 #pragma unroll
         for (int t = 0; t < NA; ++t)
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const float cr = cur[t][e].x, ci = cur[t][e].y;
-                aE[e] += fmaf(cr, cr, ci * ci);
-                if (!FIRST) {
-                    aR[e] += fmaf(cr, dr[t][e], ci * di[t][e]);
-                    aI[e] += fmaf(ci, dr[t][e], -(cr * di[t][e]));
-                }
+                const pf2 c = pf2{cur[t][e].x, cur[t][e].y};
+                aE[e] += fmaf(c.x, c.x, c.y * c.y);
+                if (!FIRST) av[e] = mulc_acc(c, d[t][e], av[e]);
             }
         // ---- in-lane partials (forward f, backward g), fp64 wave scan ----
-        float fR[E], fI[E], fE[E], gR[E], gI[E], gE[E];
-        fR[0] = aR[0]; fI[0] = aI[0]; fE[0] = aE[0];
+        pf2 fS[E], gS[E];
+        float fE[E], gE[E];
+        fS[0] = av[0]; fE[0] = aE[0];
 #pragma unroll
-        for (int e = 1; e < E; ++e) { fR[e] = fR[e - 1] + aR[e]; fI[e] = fI[e - 1] + aI[e]; fE[e] = fE[e - 1] + aE[e]; }
-        gR[E - 1] = 0.f; gI[E - 1] = 0.f; gE[E - 1] = 0.f;
+        for (int e = 1; e < E; ++e) { fS[e] = fS[e - 1] + av[e]; fE[e] = fE[e - 1] + aE[e]; }
+        gS[E - 1] = pf2{0.f, 0.f}; gE[E - 1] = 0.f;
 #pragma unroll
-        for (int e = E - 2; e >= 0; --e) { gR[e] = gR[e + 1] + aR[e + 1]; gI[e] = gI[e + 1] + aI[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
+        for (int e = E - 2; e >= 0; --e) { gS[e] = gS[e + 1] + av[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
         const RowScan se_ = row_scan(fE[E - 1]);
         const double tE = se_.tot;
         const float xE = se_.x, uE = se_.u;
         double tR = 0.0, tI = 0.0;
-        float xR = 0.f, xI = 0.f, uR = 0.f, uI = 0.f;
+        pf2 xS = pf2{0.f, 0.f}, uS = pf2{0.f, 0.f};
         if (!FIRST) {                                        // no lagged product before row MR
-            const RowScan sr_ = row_scan(fR[E - 1]), si_ = row_scan(fI[E - 1]);
+            const RowScan sr_ = row_scan(fS[E - 1].x), si_ = row_scan(fS[E - 1].y);
             tR = sr_.tot; tI = si_.tot;
-            xR = sr_.x; xI = si_.x;
-            uR = sr_.u; uI = si_.u;
+            xS = pf2{sr_.x, si_.x};
+            uS = pf2{sr_.u, si_.u};
         }
-        const float wR = (float)(FIRST ? CR : CR - cbR[so]);
-        const float wI = (float)(FIRST ? CI : CI - cbI[so]);
+        const pf2 wS = FIRST ? pf2{(float)CR, (float)CI} : pf2{(float)(CR - cbR[so]), (float)(CI - cbI[so])};
         const float wE = (float)(FIRST ? CE : CE - cbE[so]);
         // ---- window sums P = suffix(row k-MR) + rows between + prefix(row k) ----
         float pr[E], pi[E], rf[E], mf[E], pmf[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            float PR = wR + (xR + fR[e]), PI = wI + (xI + fI[e]), RR = wE + (xE + fE[e]);
-            if (!FIRST) { PR += sR[sl][e]; PI += sI[sl][e]; RR += sE[sl][e]; }
-            sR[sl][e] = uR + gR[e]; sI[sl][e] = uI + gI[e]; sE[sl][e] = uE + gE[e];
-            const float pm = fmaf(PR, PR, PI * PI);
+            pf2 P = wS + (xS + fS[e]);
+            float RR = wE + (xE + fE[e]);
+            if (!FIRST) { P += sS[sl][e]; RR += sE[sl][e]; }
+            sS[sl][e] = uS + gS[e]; sE[sl][e] = uE + gE[e];
+            const float pm = fmaf(P.x, P.x, P.y * P.y);
             float m = 0.f;
             if (!FIRST && RR > floor_) m = fminf(pm * __builtin_amdgcn_rcpf(RR * RR), 1.f);
-            pr[e] = PR; pi[e] = PI; rf[e] = RR; mf[e] = m; pmf[e] = pm;
+            pr[e] = P.x; pi[e] = P.y; rf[e] = RR; mf[e] = m; pmf[e] = pm;
         }
         cbR[so] = CR + tR; cbI[so] = CI + tI; cbE[so] = CE + tE;
         CR += tR; CI += tI; CE += tE;
@@ -482,9 +491,9 @@ __global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
         s.cbR[m] = 0.0; s.cbI[m] = 0.0; s.cbE[m] = 0.0;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            s.sR[m][e] = 0.f; s.sI[m][e] = 0.f; s.sE[m][e] = 0.f;
+            s.sS[m][e] = pf2{0.f, 0.f}; s.sE[m][e] = 0.f;
 #pragma unroll
-            for (int t = 0; t < (S::LDSLAG ? 1 : NA); ++t) { s.lr[t][m][e] = 0.f; s.li[t][m][e] = 0.f; }
+            for (int t = 0; t < (S::LDSLAG ? 1 : NA); ++t) s.lx[t][m][e] = pf2{0.f, 0.f};
         }
     }
 #pragma unroll
@@ -604,5 +613,7 @@ int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipS
         if (E == 2) return n_ant == 1 ? launch_stream_mr<2, 1>(mr, a, st) : launch_stream_mr<2, 2>(mr, a, st);
         return n_ant == 1 ? launch_stream_mr<4, 1>(mr, a, st) : launch_stream_mr<4, 2>(mr, a, st);
     }
+    // detect-only keeps the full call's E (events identical to the full call's, same arithmetic);
+    // E = 4 would be ~8 % faster there (paired A/B r02w: 0.134 -> 0.119 ms)
     return n_ant == 1 ? launch_e<1>(plan / 10, plan % 10, a, st) : launch_e<2>(plan / 10, plan % 10, a, st);
 }
