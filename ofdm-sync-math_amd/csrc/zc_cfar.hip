@@ -1,0 +1,294 @@
+// zc_cfar.hip — zc_v2 CFAR + gate (zc_v2.py:300-346 + :374-446), fused, lane-per-stream recursion.
+//
+// The only sequential part of zc_streaming_detection is the reference's running sum
+// (RunningSum.step, zc_v2.py:219-238): acc = (acc + c[i]) - c[i-W] in float64, left to right.
+// Its rounding does not commute, so it is evaluated exactly in that order — but by ONE LANE PER
+// STREAM: a workgroup owns ZS = 16 streams, and 16 lanes of its wave 0 (the walker) advance the 16
+// recursions together, one sample per step (2 dependent v_add_f64).  Everything else is parallel
+// over samples and runs in the other three waves of the workgroup, one chunk behind the walker:
+// the threshold flags (corr_scaled >= thresh_scaled, |c| >= min), the stores of every state
+// array (coalesced 64-sample rows), and the gate machine in closed form.
+//
+// Chunks of ZC = 64·ZR samples, staged through LDS (global -> registers -> LDS, two chunks ahead):
+//   c tiles (3 buffers: walker reads chunk q while the helpers read chunk q-1 and chunk q+1 lands),
+//   c[i-W] tiles (2 buffers, walker only), running-sum tiles (2 buffers, walker -> helpers).
+// One barrier per chunk.
+//
+// Gate (zc_v2.py:374-446) in closed form over the valid samples (valid = i >= W is a prefix):
+// with Hp = max(H, 1) and prev(n) the last above sample < n, an open gate closes at the first
+// non-above n with n - prev(n) = Hp (the low counter reaches H - 1 before it), and an above
+// sample opens a gate iff it is the first one or its gap to prev exceeds Hp (the previous gate
+// has closed).  For Hp >= 64 (one row) a row holds at most one close (the carried gate's, at
+// prev + Hp, before any above sample of the row) and then at most one open (its first above
+// sample).  The peak is the first maximum of c over [gate_start, gate_end] (strict >, the
+// opening sample first); gate_mask marks (gate_start, gate_end], and [gate_start, n) for a gate
+// still open at the end.  Shorter hysteresis runs the sequential kernel of corr.hip.
+#include "ofs_common.h"
+#include "ofdmsync.h"
+
+using namespace ofs;
+
+namespace {
+
+#ifndef OFS_ZC_S
+#define OFS_ZC_S 8
+#endif
+constexpr int ZS = OFS_ZC_S;      // streams per workgroup (walker lanes)
+#ifndef OFS_ZC_R
+#define OFS_ZC_R 2
+#endif
+// diagnostic builds: OFS_ZC_NOWALK / OFS_ZC_NOHELP skip the walker / the helpers (timing only)
+#ifndef OFS_ZC_NOWALK
+#define OFS_ZC_NOWALK 0
+#endif
+#ifndef OFS_ZC_NOCHAIN
+#define OFS_ZC_NOCHAIN 0
+#endif
+#ifndef OFS_ZC_NOHELP
+#define OFS_ZC_NOHELP 0
+#endif
+constexpr int ZR = OFS_ZC_R;      // 64-sample rows of the gate machine per chunk
+constexpr int ZC = 64 * ZR;       // samples per chunk
+constexpr int ZP = ZC + 2;        // LDS row pitch in doubles (16-byte rows; walker column reads spread over banks)
+constexpr int ZH = 3;             // helper waves
+
+struct ZcArgs {
+    const double* mag;
+    int64_t B, n;
+    int W; double tv, scale, minmag; int reflen, Hp;
+    double* local_sum; double* corr_scaled; double* thresh_scaled;
+    uint8_t* above; uint8_t* valid; uint8_t* gate_mask;
+    int max_ev; int32_t* n_ev; int64_t* ev; double* ev_v;
+};
+
+// per-stream gate state, wave-uniform in the helper wave that owns the stream
+struct ZGate {
+    int64_t last_above;     // last above sample (< current row), -1 if none
+    int64_t gs, pk;
+    double pv;
+    int open, nev;
+};
+
+__global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
+#pragma clang fp contract(off)
+    __shared__ double tc[3][ZS][ZP];      // c
+    __shared__ double to[2][ZS][ZP];      // c[i - W] (0 before the window fills)
+    __shared__ double ta[2][ZS][ZP];      // running sum after sample i
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t b0 = (int64_t)blockIdx.x * ZS;
+    const int ns = (int)min((int64_t)ZS, a.B - b0);          // streams of this workgroup
+    const int64_t n = a.n;
+    const int nch = (int)((n + ZC - 1) / ZC);
+
+    // loader = the walker wave, which issues no global stores: its wait for the loads of the next
+    // chunk (staged one iteration after they are issued) never drains the helpers' stores
+    // loader = the walker wave, which issues no global stores: its wait for the loads of the next
+    // chunk (staged one iteration after they are issued) never drains the helpers' stores.
+    // (Two register sets, loads two chunks ahead: measured slower, 0.64 vs 0.46 ms.)
+    double pc[ZR][ZS], po[ZR][ZS];
+    const double* cw = a.mag + b0 * n;                        // this workgroup's streams
+    auto load = [&](int q) {
+#pragma unroll
+        for (int rr = 0; rr < ZR; ++rr) {
+            const int64_t i = (int64_t)q * ZC + 64 * rr + lane;
+#pragma unroll
+            for (int s = 0; s < ZS; ++s) {
+                const bool ok = s < ns && i < n;
+                pc[rr][s] = ok ? cw[s * n + i] : 0.0;
+                po[rr][s] = (ok && i >= a.W) ? cw[s * n + i - a.W] : 0.0;
+            }
+        }
+    };
+    auto stage = [&](int q) {
+#pragma unroll
+        for (int rr = 0; rr < ZR; ++rr)
+#pragma unroll
+            for (int s = 0; s < ZS; ++s) {
+                tc[q % 3][s][64 * rr + lane] = pc[rr][s];
+                to[q & 1][s][64 * rr + lane] = po[rr][s];
+            }
+    };
+
+    ZGate g[(ZS + ZH - 1) / ZH];
+#pragma unroll
+    for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) { g[j].last_above = -1; g[j].gs = 0; g[j].pk = 0; g[j].pv = 0.0; g[j].open = 0; g[j].nev = 0; }
+    double acc = 0.0;                                         // walker lane s < ns: stream b0 + s
+
+    // LDS-only barrier: the helpers' global stores are never waited for (a __syncthreads() fence
+    // would drain them, a full store round trip per chunk); the loads are staged one iteration
+    // after they are issued, so their wait overlaps a whole chunk of work
+    auto lds_barrier = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
+    if (wv == 0) {
+        load(0);
+        stage(0);
+        if (1 < nch) load(1);
+    }
+    lds_barrier();
+    for (int q = 0; q <= nch; ++q) {
+        if (wv == 0) {
+            if (q + 1 < nch) stage(q + 1);                    // loaded during the previous chunk
+            if (q + 2 < nch) load(q + 2);
+        }
+        if (wv == 0) {
+            // ---- walker: the exact left-to-right recursion of RunningSum.step ----
+            if (!OFS_ZC_NOWALK && q < nch && lane < ZS) {
+                const int cnt = (int)min((int64_t)ZC, n - (int64_t)q * ZC);
+                const double* x = tc[q % 3][lane];
+                const double* o = to[q & 1][lane];
+                double* r = ta[q & 1][lane];
+                if (cnt == ZC) {
+                    // LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per
+                    // sample; an LDS round trip per sample would set the pace instead)
+                    constexpr int ZB = 8;
+                    double2 xv[ZB / 2], ov[ZB / 2];
+#pragma unroll
+                    for (int j = 0; j < ZB / 2; ++j) {
+                        xv[j] = reinterpret_cast<const double2*>(x)[j];
+                        ov[j] = reinterpret_cast<const double2*>(o)[j];
+                    }
+#pragma unroll
+                    for (int bb = 0; bb < ZC / ZB; ++bb) {
+                        double2 xn[ZB / 2], on[ZB / 2];
+                        if (bb + 1 < ZC / ZB) {
+#pragma unroll
+                            for (int j = 0; j < ZB / 2; ++j) {
+                                xn[j] = reinterpret_cast<const double2*>(x + (bb + 1) * ZB)[j];
+                                on[j] = reinterpret_cast<const double2*>(o + (bb + 1) * ZB)[j];
+                            }
+                        }
+#pragma unroll
+                        for (int j = 0; j < ZB / 2; ++j) {
+                            double2 rr;
+#if OFS_ZC_NOCHAIN
+                            rr.x = xv[j].x - ov[j].x; rr.y = xv[j].y - ov[j].y;
+#else
+                            acc = (acc + xv[j].x) - ov[j].x; rr.x = acc;
+                            acc = (acc + xv[j].y) - ov[j].y; rr.y = acc;
+#endif
+                            reinterpret_cast<double2*>(r + bb * ZB)[j] = rr;
+                        }
+                        if (bb + 1 < ZC / ZB) {
+#pragma unroll
+                            for (int j = 0; j < ZB / 2; ++j) { xv[j] = xn[j]; ov[j] = on[j]; }
+                        }
+                    }
+                } else {
+                    for (int u = 0; u < cnt; ++u) { acc = (acc + x[u]) - o[u]; r[u] = acc; }
+                }
+            }
+        } else if (!OFS_ZC_NOHELP && q >= 1) {
+            // ---- helpers: chunk q-1 (flags, stores, gate) ----
+            const int qc = q - 1;
+#pragma unroll
+            for (int rr = 0; rr < ZR; ++rr) {
+            const int64_t base = (int64_t)qc * ZC + 64 * rr;
+            const int64_t i = base + lane;
+            const bool inb = i < n;
+            const bool vd = inb && i >= a.W;
+#pragma unroll
+            for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) {
+                const int s = (wv - 1) + ZH * j;
+                if (s >= ns) break;
+                ZGate& G = g[j];
+                const double c = tc[qc % 3][s][64 * rr + lane];
+                const double ls = ta[qc & 1][s][64 * rr + lane];
+                const double cs = c * a.scale, th = ls * a.tv;
+                const bool ab = vd && (cs >= th) && (c >= a.minmag);
+                const uint64_t abm = __ballot(ab);
+                const int64_t o = (b0 + s) * n + i;
+                // gate in closed form (Hp >= 64): carried close first, then this row's first above
+                int close_l = -1;                                     // row lane of the close
+                if (G.open) {
+                    const int64_t nc = G.last_above + a.Hp;
+                    const int64_t fa = abm ? base + __builtin_ctzll(abm) : INT64_MAX;
+                    if (nc >= base && nc < base + 64 && nc < n && fa > nc) close_l = (int)(nc - base);
+                }
+                const int open_l = abm ? __builtin_ctzll(abm) : -1;
+                const bool carried = G.open != 0;
+                const bool opens = open_l >= 0 && (!carried || close_l >= 0);   // Hp >= 64: open after close
+                // gate_mask: carried gate over [0, close] (or the whole row), new gate over (open, 63]
+                const int cend = carried ? (close_l >= 0 ? close_l : 63) : -1;
+                const bool mk = inb && ((lane <= cend) || (opens && lane > open_l));
+                if (carried) {                                       // peak over [0, cend]
+                    const double v = (inb && lane <= cend) ? c : -__builtin_huge_val();
+                    const double m = wave_max(v);
+                    if (m > G.pv) {
+                        const uint64_t at = __ballot(inb && lane <= cend && c == m);
+                        G.pv = m; G.pk = base + __builtin_ctzll(at);
+                    }
+                    if (close_l >= 0) {
+                        if (a.ev && G.nev < a.max_ev && lane < 4) {
+                            int64_t* r = a.ev + ((b0 + s) * (int64_t)a.max_ev + G.nev) * 4;
+                            const int64_t ds = G.pk - a.reflen + 1 > 0 ? G.pk - a.reflen + 1 : 0;
+                            r[lane] = lane == 0 ? G.pk : lane == 1 ? G.gs : lane == 2 ? base + close_l : ds;
+                            if (lane == 0 && a.ev_v) a.ev_v[(b0 + s) * (int64_t)a.max_ev + G.nev] = G.pv;
+                        }
+                        G.nev += 1; G.open = 0; G.pv = 0.0;
+                    }
+                }
+                if (opens) {                                         // opening sample, then (open, 63]
+                    G.open = 1; G.gs = base + open_l; G.pk = G.gs;
+                    G.pv = readlane(c, open_l);
+                    const double v = (inb && lane > open_l) ? c : -__builtin_huge_val();
+                    const double m = wave_max(v);
+                    if (m > G.pv) {
+                        const uint64_t at = __ballot(inb && lane > open_l && c == m);
+                        G.pv = m; G.pk = base + __builtin_ctzll(at);
+                    }
+                }
+                if (abm) G.last_above = base + 63 - __builtin_clzll(abm);
+                if (inb) {
+                    if (a.local_sum) a.local_sum[o] = ls;
+                    if (a.corr_scaled) a.corr_scaled[o] = cs;
+                    if (a.thresh_scaled) a.thresh_scaled[o] = th;
+                    if (a.above) a.above[o] = (uint8_t)ab;
+                    if (a.valid) a.valid[o] = (uint8_t)vd;
+                    if (a.gate_mask) a.gate_mask[o] = (uint8_t)mk;
+                }
+            }
+            }
+        }
+        lds_barrier();
+    }
+    // ---- gates still open at the end: gate_end = n, gate_mask[gate_start:n] ----
+    if (wv >= 1) {
+#pragma unroll
+        for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) {
+            const int s = (wv - 1) + ZH * j;
+            if (s >= ns) break;
+            ZGate& G = g[j];
+            if (G.open) {
+                if (a.ev && G.nev < a.max_ev && lane < 4) {
+                    int64_t* r = a.ev + ((b0 + s) * (int64_t)a.max_ev + G.nev) * 4;
+                    const int64_t ds = G.pk - a.reflen + 1 > 0 ? G.pk - a.reflen + 1 : 0;
+                    r[lane] = lane == 0 ? G.pk : lane == 1 ? G.gs : lane == 2 ? n : ds;
+                    if (lane == 0 && a.ev_v) a.ev_v[(b0 + s) * (int64_t)a.max_ev + G.nev] = G.pv;
+                }
+                G.nev += 1;
+                if (lane == 0 && a.gate_mask) a.gate_mask[(b0 + s) * n + G.gs] = 1;
+            }
+            if (lane == 0 && a.n_ev) a.n_ev[b0 + s] = G.nev;
+        }
+    }
+}
+
+}  // namespace
+
+// fused CFAR + gate for hysteresis >= one chunk; returns 0 when the shape is not covered
+int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double tv, double scale,
+                    double minmag, int reflen, int hyst, double* local_sum, double* corr_scaled,
+                    double* thresh_scaled, uint8_t* above, uint8_t* valid, uint8_t* gate_mask, int max_ev,
+                    int32_t* n_ev, int64_t* ev, double* ev_v, hipStream_t st) {
+    const int Hp = hyst > 1 ? hyst : 1;
+    if (Hp < 64 || B <= 0 || n <= 0 || getenv("OFS_ZC_SEQ")) return 0;
+    ZcArgs a{corr_mag, B, n, W, tv, scale, minmag, reflen, Hp, local_sum, corr_scaled, thresh_scaled,
+             above, valid, gate_mask, max_ev, n_ev, ev, ev_v};
+    const int64_t grid = (B + ZS - 1) / ZS;
+    hipLaunchKernelGGL(zc_cfar_kernel, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
+}
