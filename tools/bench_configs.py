@@ -502,24 +502,37 @@ def zc_freq_fp64(dev, st, steps, warmup):
                   B * noff * 62 * 22, "fp64")
 
 
-def zc_detect(dev, st, steps, warmup):
-    """zc_v2 CFAR + gate (zc_v2.py:300-446) on |corr| rows: B = 4096 x 16384 f64, sequential per
-    stream (one wave per stream, bit-exact left-to-right recursion); state arrays not stored."""
+def zc_detect(dev, st, steps, warmup, state=False, seq=False):
+    """zc_v2 CFAR + gate (zc_v2.py:300-446) on |corr| rows: B = 4096 x 16384 f64.  Default kernel:
+    zc_cfar_kernel (lane-per-stream exact recursion + closed-form gate, zc_cfar.hip); seq=True times
+    the sequential one-wave-per-stream kernel (OFS_ZC_SEQ).  state=True also stores the five state
+    arrays (local_sum, corr_scaled, thresh_scaled 8 B each, above, valid 1 B each)."""
     from ofdm_sync_amd import zc_v2
     B, n = 4096, 16384
     g = torch.Generator(device=dev).manual_seed(7)
     mag = torch.rand((B, n), dtype=torch.float64, device=dev, generator=g) * 0.5
     mag[:, 5000:5100] += 2.0
-    ms = timed(lambda: zc_v2._detect_run(mag, zc_v2.CORR_WINDOW_SIZE, zc_v2.THRESH_VALUE, zc_v2.THRESH_FRAC_BITS,
-                                         zc_v2.MIN_CORR_MAG, 2048, zc_v2.HYSTERESIS, 4, want_state=False),
-               steps, warmup, st)
-    return dict(config="zc_detect", workload=f"zc_v2 CFAR + gate, {B} x {n} f64 |corr| (events + gate mask)",
-                kernel="zc_detect_kernel (one wave per stream, sequential recursion)", samples=B * n, ms=ms,
-                alg_bytes=B * n * (8 + 1), bytes_per_sample="8 in + gate 1 out")
+    if seq:
+        os.environ["OFS_ZC_SEQ"] = "1"
+    try:
+        ms = timed(lambda: zc_v2._detect_run(mag, zc_v2.CORR_WINDOW_SIZE, zc_v2.THRESH_VALUE, zc_v2.THRESH_FRAC_BITS,
+                                             zc_v2.MIN_CORR_MAG, 2048, zc_v2.HYSTERESIS, 4, want_state=state),
+                   steps, warmup, st)
+    finally:
+        os.environ.pop("OFS_ZC_SEQ", None)
+    name = "zc_detect" + ("_state" if state else "") + ("_seq" if seq else "")
+    return dict(config=name, workload=f"zc_v2 CFAR + gate, {B} x {n} f64 |corr| (events + gate mask"
+                + (" + state arrays)" if state else ")"),
+                kernel=("zc_detect_kernel (one wave per stream, sequential recursion)" if seq else
+                        "zc_cfar_kernel (8 streams per workgroup: lane-per-stream recursion + closed-form gate)"),
+                samples=B * n, ms=ms, alg_bytes=B * n * (8 + 1 + (26 if state else 0)),
+                bytes_per_sample="8 in + gate 1 out" + (" + 3 x 8 + 2 x 1 state out" if state else ""))
 
 
 CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "park_fp32": park, "park_fp64": lambda *a, **k: park(*a, prec="fp64", **k), "zc_mf": zc_mf,
            "zc_freq_fp64": zc_freq_fp64, "zc_detect": zc_detect,
+           "zc_detect_state": lambda *a, **k: zc_detect(*a, state=True, **k),
+           "zc_detect_seq": lambda *a, **k: zc_detect(*a, seq=True, **k),
            "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
            "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
