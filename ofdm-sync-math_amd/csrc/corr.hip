@@ -64,7 +64,20 @@ __host__ __device__ constexpr int64_t split_stride(int64_t len) { return (len + 
 // rotate through a ring whose slot is (q ∓ k) mod OPT, resolved at compile time by
 // unrolling k by OPT.
 // ------------------------------------------------------------------------------------------
-template <int FMT, class R>
+// Energy: the OPT outputs of a thread share all but the first / last few samples of their
+// windows, so (SPLIT, half >= OPT) E_q = C + H_q + T_q with C = Σ_{k=OPT-1}^{half-1} |x[d0+k]|²
+// (accumulated once, from output 0's forward values), H_q = Σ_{k=q}^{OPT-2} |x[d0+k]|² and
+// T_q = Σ_{k=half}^{half+q-1} |x[d0+k]|² — sums of non-negative terms only, 2 instead of 2·OPT FMAs
+// per step.
+// (packed forms of the complex MAC measured no faster for fp32 - vector-type swizzles 3.95 ms, two
+// inline-asm v_pk_fma_f32 with op_sel 2.67 ms, against 2.51 ms for the scalar FMAs: r02ab)
+template <class R, class V>
+__device__ __forceinline__ void park_mac(const V& b, const V& f, R& pr, R& pi) {
+    pr = fma(b.x, f.x, fma(-b.y, f.y, pr));
+    pi = fma(b.x, f.y, fma(b.y, f.x, pi));
+}
+
+template <int FMT, class R, bool SPLIT>
 __global__ __launch_bounds__(CW) void park_kernel(const void* x, int64_t T, int nb, int half,
                                                   int64_t nout, R* __restrict__ Mo,
                                                   R* __restrict__ Po, R* __restrict__ Eo) {
@@ -100,6 +113,7 @@ __global__ __launch_bounds__(CW) void park_kernel(const void* x, int64_t T, int 
         V bw[OPT], fw[OPT];
 #pragma unroll
         for (int q = 0; q < OPT; ++q) { bw[q] = at(c0 + q); fw[q] = at(c0 + q); }
+        R ce = 0;                                         // SPLIT: C of this branch
         for (int kk = 0; kk < ksteps; kk += OPT) {
 #pragma unroll
             for (int u = 0; u < OPT; ++u) {
@@ -109,9 +123,12 @@ __global__ __launch_bounds__(CW) void park_kernel(const void* x, int64_t T, int 
                     for (int q = 0; q < OPT; ++q) {
                         const V bq = bw[(q - u + OPT) % OPT];
                         const V fq = fw[(q + u) % OPT];
-                        pr[q] = fma(bq.x, fq.x, fma(-bq.y, fq.y, pr[q]));
-                        pi[q] = fma(bq.x, fq.y, fma(bq.y, fq.x, pi[q]));
-                        en[q] = fma(fq.x, fq.x, fma(fq.y, fq.y, en[q]));
+                        park_mac<R, V>(bq, fq, pr[q], pi[q]);
+                        if (!SPLIT) en[q] = fma(fq.x, fq.x, fma(fq.y, fq.y, en[q]));
+                    }
+                    if (SPLIT && (kk > 0 || u >= OPT - 1)) {
+                        const V f0 = fw[u % OPT];         // x[d0 + k]
+                        ce = fma(f0.x, f0.x, fma(f0.y, f0.y, ce));
                     }
                 }
                 // next step: new backward x[d0+OPT t-(k+1)] into slot of b_{OPT-1},
@@ -119,6 +136,23 @@ __global__ __launch_bounds__(CW) void park_kernel(const void* x, int64_t T, int 
                 bw[(OPT - 1 - u + OPT) % OPT] = at(c0 - (k + 1));
                 fw[u % OPT] = at(c0 + OPT + k);
             }
+        }
+        if constexpr (SPLIT) {
+            R hd[OPT], tl[OPT];                           // |x[d0+k]|², |x[d0+half+k]|², k < OPT-1
+#pragma unroll
+            for (int k = 0; k < OPT - 1; ++k) {
+                const V h = at(c0 + k), w = at(c0 + half + k);
+                hd[k] = fma(h.x, h.x, h.y * h.y);
+                tl[k] = fma(w.x, w.x, w.y * w.y);
+            }
+            R hs = 0, ts = 0;
+#pragma unroll
+            for (int q = OPT - 1; q >= 0; --q) {          // H_q: suffix of hd from q
+                en[q] += ce + hs;
+                if (q > 0) hs += hd[q - 1];
+            }
+#pragma unroll
+            for (int q = 1; q < OPT; ++q) { ts += tl[q - 1]; en[q] += ts; }   // T_q
         }
     }
 #pragma unroll
@@ -286,28 +320,67 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
 #pragma unroll
     for (int r = 0; r < NB; ++r) { Wr[r] = 0.0; Wi[r] = 0.0; }
 
-    // ---- initial window W_k(s0) = Σ_{j=s0}^{s0+N-1} x[j] w^{kj}
+    // ---- initial window W_k(s0) = Σ_{j=s0}^{s0+N-1} x[j] w^{kj}: four independent accumulator /
+    // twiddle chains (samples j = 4m + p) so the dependent FMA and twiddle recurrences overlap
+    const double2 wk4 = twiddle((4 * (int64_t)kb) % N, N);
+    const double2 wkp[3] = {wk, twiddle((2 * (int64_t)kb) % N, N), twiddle((3 * (int64_t)kb) % N, N)};
     const int64_t s0 = o0 + a.cp;
-    for (int64_t j0 = s0; j0 < s0 + N; j0 += 64) {
-        const int cnt = (int)min((int64_t)64, s0 + N - j0);
-        double xr[NB], xi[NB];
+    {
+        double Pr[4][NB], Pi[4][NB];
 #pragma unroll
-        for (int r = 0; r < NB; ++r) {
-            double2 v = make_double2(0.0, 0.0);
-            if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
-            xr[r] = v.x; xi[r] = v.y;
-        }
-        double2 tw = twiddle(((int64_t)kb * j0) % N, N);
-        for (int u = 0; u < cnt; ++u) {
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int r = 0; r < NB; ++r) { Pr[p][r] = 0.0; Pi[p][r] = 0.0; }
+        for (int64_t j0 = s0; j0 < s0 + N; j0 += 64) {
+            const int cnt = (int)min((int64_t)64, s0 + N - j0);
+            double xr[NB], xi[NB];
 #pragma unroll
             for (int r = 0; r < NB; ++r) {
-                const double ur = ofs::readlane(xr[r], u), ui = ofs::readlane(xi[r], u);
-                Wr[r] = fma(ur, tw.x, fma(-ui, tw.y, Wr[r]));
-                Wi[r] = fma(ur, tw.y, fma(ui, tw.x, Wi[r]));
+                double2 v = make_double2(0.0, 0.0);
+                if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
+                xr[r] = v.x; xi[r] = v.y;
             }
-            const double nr = tw.x * wk.x - tw.y * wk.y;
-            const double ni = tw.x * wk.y + tw.y * wk.x;
-            tw.x = nr; tw.y = ni;
+            double2 tw[4];
+            tw[0] = twiddle(((int64_t)kb * j0) % N, N);                 // exact anchor per block
+#pragma unroll
+            for (int p = 1; p < 4; ++p)
+                tw[p] = make_double2(tw[0].x * wkp[p - 1].x - tw[0].y * wkp[p - 1].y,
+                                     tw[0].x * wkp[p - 1].y + tw[0].y * wkp[p - 1].x);
+            if (cnt == 64) {
+#pragma unroll 4
+                for (int u = 0; u < 64; u += 4) {
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                        for (int r = 0; r < NB; ++r) {
+                            const double ur = ofs::readlane(xr[r], u + p), ui = ofs::readlane(xi[r], u + p);
+                            Pr[p][r] = fma(ur, tw[p].x, fma(-ui, tw[p].y, Pr[p][r]));
+                            Pi[p][r] = fma(ur, tw[p].y, fma(ui, tw[p].x, Pi[p][r]));
+                        }
+                        const double nr = tw[p].x * wk4.x - tw[p].y * wk4.y;
+                        const double ni = tw[p].x * wk4.y + tw[p].y * wk4.x;
+                        tw[p].x = nr; tw[p].y = ni;
+                    }
+                }
+            } else {
+                double2 t = tw[0];
+                for (int u = 0; u < cnt; ++u) {
+#pragma unroll
+                    for (int r = 0; r < NB; ++r) {
+                        const double ur = ofs::readlane(xr[r], u), ui = ofs::readlane(xi[r], u);
+                        Pr[0][r] = fma(ur, t.x, fma(-ui, t.y, Pr[0][r]));
+                        Pi[0][r] = fma(ur, t.y, fma(ui, t.x, Pi[0][r]));
+                    }
+                    const double nr = t.x * wk.x - t.y * wk.y;
+                    const double ni = t.x * wk.y + t.y * wk.x;
+                    t.x = nr; t.y = ni;
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            Wr[r] = (Pr[0][r] + Pr[1][r]) + (Pr[2][r] + Pr[3][r]);
+            Wi[r] = (Pi[0][r] + Pi[1][r]) + (Pi[2][r] + Pi[3][r]);
         }
     }
 
@@ -816,7 +889,9 @@ static int park_launch(const void* x, int64_t B, int nb, int64_t T, int half, in
                        void* M, void* P, void* E, hipStream_t st) {
     const int64_t len = CD + 2 * (int64_t)half - 2 + 2 * PADF;
     const size_t lds = (size_t)split_stride(len) * OPT * sizeof(typename C2<R>::T);
-    auto k = park_kernel<FMT, R>;
+    // shared-window energy needs half >= OPT - 1 (OFS_PARK_DIRECT=1: per-output energy sums, A/B)
+    static const bool direct = getenv("OFS_PARK_DIRECT") != nullptr;
+    auto k = (half >= OPT - 1 && !direct) ? park_kernel<FMT, R, true> : park_kernel<FMT, R, false>;
     const int rc = set_lds(k, lds);
     if (rc) return rc;
     const dim3 grid((unsigned)((nout + CD - 1) / CD), (unsigned)B);
@@ -904,6 +979,12 @@ static int zf_launch(const ZfArgs& a, int nb, hipStream_t st) {
 }
 
 }  // namespace
+
+// zc_cfar.hip
+int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double tv, double scale,
+                    double minmag, int reflen, int hyst, double* local_sum, double* corr_scaled,
+                    double* thresh_scaled, uint8_t* above, uint8_t* valid, uint8_t* gate_mask, int max_ev,
+                    int32_t* n_ev, int64_t* ev, double* ev_v, hipStream_t st);
 
 extern "C" {
 
@@ -1022,6 +1103,11 @@ int32_t ofs_zc_detect(const double* corr_mag, int64_t B, int64_t n, int32_t wind
     a.local_sum = local_sum; a.corr_scaled = corr_scaled; a.thresh_scaled = thresh_scaled;
     a.above = above_threshold; a.valid = metric_valid; a.gate_mask = gate_mask;
     a.max_ev = max_events; a.n_ev = n_events; a.ev = ev_int; a.ev_v = ev_peak;
+    // hysteresis >= 64: fused lane-per-stream recursion + closed-form gate (zc_cfar.hip)
+    const int frc = ofs_zc_cfar_try(corr_mag, B, n, a.W, a.tv, a.scale, a.minmag, a.reflen, a.hyst, local_sum,
+                                    corr_scaled, thresh_scaled, above_threshold, metric_valid, gate_mask,
+                                    max_events, n_events, ev_int, ev_peak, (hipStream_t)stream);
+    if (frc != 0) return frc > 0 ? OFS_OK : frc;
     hipLaunchKernelGGL(zc_detect_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
