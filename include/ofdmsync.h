@@ -170,7 +170,7 @@ int32_t ofs_sc_minn_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
 /*
  * Which kernel a window-metric call runs on: kind 1 = ofs_sc_metric r_mode 0, 2 = r_mode 1,
  * 3 = ofs_minn_metric, 4 = ofs_sc_minn_metric.  Returns 10*E + MW of the streaming fp32 fast kernel (win_fast.hip:
- * complex64, 1-2 branches, even T, window of MW rows of 64*E samples), or 0 for the general
+ * complex64, 1-2 branches, any T >= N, window of MW rows of 64*E samples), or 0 for the general
  * LDS-tiled engine.
  */
 int32_t ofs_win_plan(int32_t kind, int32_t in_fmt, int32_t precision, int32_t n_br, int64_t T,

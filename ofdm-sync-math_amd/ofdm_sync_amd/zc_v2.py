@@ -6,8 +6,10 @@ zc_streaming_detection      zc_v2.py:300-346  -> ofs_zc_detect (flags only)
 detect_zc_peaks             zc_v2.py:374-446  -> ofs_zc_gate
 detect_zc_preamble          zc_v2.py:452-519  -> ofs_zc_correlate (OFS_ZC_V2 / OFS_ZC_SUM,
                                                  |corr| fused) + ofs_zc_detect (CFAR + gate fused)
-The correlation is an LDS-tiled direct sum in fp64 (csrc/corr.hip); the CFAR running sum
-and the gate are the reference's sequential float64 recursion, one wave per stream.
+The correlation is an LDS-tiled direct sum in fp64 (csrc/corr.hip) or, from 256 taps, FFT
+overlap-save (csrc/zc_fftcorr.hip); the CFAR running sum is the reference's sequential float64
+recursion evaluated one lane per stream and the gate a closed-form machine over 64-sample rows
+(csrc/zc_cfar.hip; hysteresis < 64 and detect_zc_peaks on a given state: one wave per stream).
 ``build_pss_symbol`` is host-side setup of the reference waveform (zc_v2.py:170-185).
 """
 from __future__ import annotations
