@@ -347,10 +347,21 @@ int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, 
  * spectrum never reaches HBM.  prune_bins == 0: the dense plan. */
 int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                 int32_t prune_bins, void** plan_out, size_t* work_bytes);
+/* As ofs_zc_fft_plan_create2, executed in chunks of chunk_windows windows (0 = all n_windows in
+ * one execution; a multiple of n_br at execute time): each chunk is one rocFFT execution into the
+ * same [chunk][N] (or [chunk][prune_bins]) `spectrum` buffer followed by its gather, so the
+ * spectrum the FFT writes is re-read from the Infinity Cache instead of HBM when chunk * N * esz
+ * is well inside its 256 MiB.  ofs_zc_fft_plan_chunk returns the windows per execution (the
+ * spectrum buffer's row count). */
+int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, int64_t chunk_windows, void** plan_out,
+                                size_t* work_bytes);
+int64_t ofs_zc_fft_plan_chunk(const void* plan);
 int32_t ofs_zc_fft_plan_destroy(void* plan);
 /*
  * For each offset off in [0, T-(N+cp)]: one batched rocFFT of x[b][br][off+cp : off+cp+N] into
- * `spectrum` ([B*n_br][N], device scratch), then one gather kernel: metric[b][off] =
+ * `spectrum` ([chunk][N] device scratch, chunk = ofs_zc_fft_plan_chunk = B*n_br unless the plan
+ * is chunked), then one gather kernel: metric[b][off] =
  * |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum |bins|^2, 1e-12), bins at the reference's
  * fftshift positions (N/2 + bin_indices) % N.  bin_indices [n_bins] int32, template_bins [n_bins]
  * c128: HOST pointers (n_bins <= 64).  metric [B][n_off]; peak_index [B] int64 / peak_value [B]

@@ -53,7 +53,9 @@ __device__ void* zc_store_cb_f32_ptr = (void*)zc_store_cb_f32;
 __device__ void* zc_store_cb_f64_ptr = (void*)zc_store_cb_f64;
 
 struct ZcFftPlan {
-    rocfft_plan plan = nullptr;
+    rocfft_plan plan = nullptr;     // `chunk` windows per execution
+    rocfft_plan tail = nullptr;     // the last n_windows % chunk windows (chunked plans only)
+    int64_t chunk = 0;              // windows per rocFFT execution (= n_windows unless chunked)
     int32_t precision = 0;
     int32_t N = 0;
     int64_t n_windows = 0;
@@ -67,7 +69,7 @@ struct ZcFftPlan {
 
 struct GatherArgs {
     const void* spec;           // [B][n_br][N] c64 | c128 (unshifted spectrum of one offset)
-    int64_t B, n_off, off;
+    int64_t B, n_off, off, b0;  // B streams of this execution, the first being stream b0
     int32_t n_br, N, n_bins;
     double e_t;
     void* metric;               // [B][n_off] f32 | f64
@@ -108,8 +110,8 @@ __global__ __launch_bounds__(ZWG) void zc_gather_kernel(GatherArgs a) {
     }
     if (lane == 0) {
         const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
-        if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[b * a.n_off + a.off] = (float)v;
-        else reinterpret_cast<double*>(a.metric)[b * a.n_off + a.off] = v;
+        if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[(a.b0 + b) * a.n_off + a.off] = (float)v;
+        else reinterpret_cast<double*>(a.metric)[(a.b0 + b) * a.n_off + a.off] = v;
     }
 }
 
@@ -155,40 +157,57 @@ std::once_flag g_setup;
 
 extern "C" {
 
-int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
-                                int32_t prune_bins, void** plan_out, size_t* work_bytes);
+int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, int64_t chunk_windows, void** plan_out, size_t* work_bytes);
 
 int32_t ofs_zc_fft_plan_create(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                void** plan_out, size_t* work_bytes) {
-    return ofs_zc_fft_plan_create2(precision, N, n_windows, in_dist, 0, plan_out, work_bytes);
+    return ofs_zc_fft_plan_create3(precision, N, n_windows, in_dist, 0, 0, plan_out, work_bytes);
 }
 
 int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                 int32_t prune_bins, void** plan_out, size_t* work_bytes) {
-    if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || n_windows < 1 ||
-        in_dist < N || prune_bins < 0 || prune_bins > ZB ||
-        (prune_bins > 0 && (N > 4096 || (N & (N - 1)))))
-        return OFS_EINVAL;
-    *plan_out = nullptr;
-    std::call_once(g_setup, [] { rocfft_setup(); });
+    return ofs_zc_fft_plan_create3(precision, N, n_windows, in_dist, prune_bins, 0, plan_out, work_bytes);
+}
+
+static rocfft_status make_fft_plan(int32_t precision, int32_t N, int64_t count, int64_t in_dist, rocfft_plan* out) {
     rocfft_plan_description desc = nullptr;
-    if (rocfft_plan_description_create(&desc) != rocfft_status_success) return OFS_EFFT;
+    if (rocfft_plan_description_create(&desc) != rocfft_status_success) return rocfft_status_failure;
     const size_t len = (size_t)N, stride = 1;
     rocfft_status s = rocfft_plan_description_set_data_layout(
         desc, rocfft_array_type_complex_interleaved, rocfft_array_type_complex_interleaved, nullptr, nullptr,
         1, &stride, (size_t)in_dist, 1, &stride, (size_t)N);
-    ZcFftPlan* p = new ZcFftPlan;
     if (s == rocfft_status_success)
-        s = rocfft_plan_create(&p->plan, rocfft_placement_notinplace, rocfft_transform_type_complex_forward,
+        s = rocfft_plan_create(out, rocfft_placement_notinplace, rocfft_transform_type_complex_forward,
                                precision == OFS_FP32 ? rocfft_precision_single : rocfft_precision_double, 1, &len,
-                               (size_t)n_windows, desc);
+                               (size_t)count, desc);
     rocfft_plan_description_destroy(desc);
+    return s;
+}
+
+int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
+                                int32_t prune_bins, int64_t chunk_windows, void** plan_out, size_t* work_bytes) {
+    if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || n_windows < 1 ||
+        in_dist < N || prune_bins < 0 || prune_bins > ZB || chunk_windows < 0 ||
+        (prune_bins > 0 && (N > 4096 || (N & (N - 1)))))
+        return OFS_EINVAL;
+    *plan_out = nullptr;
+    std::call_once(g_setup, [] { rocfft_setup(); });
+    ZcFftPlan* p = new ZcFftPlan;
+    p->chunk = (chunk_windows == 0 || chunk_windows > n_windows) ? n_windows : chunk_windows;
+    rocfft_status s = make_fft_plan(precision, N, p->chunk, in_dist, &p->plan);
+    if (s == rocfft_status_success && n_windows % p->chunk)
+        s = make_fft_plan(precision, N, n_windows % p->chunk, in_dist, &p->tail);
+    size_t wb = 0;
     if (s == rocfft_status_success) s = rocfft_plan_get_work_buffer_size(p->plan, &p->work_bytes);
+    if (s == rocfft_status_success && p->tail) s = rocfft_plan_get_work_buffer_size(p->tail, &wb);
     if (s != rocfft_status_success) {
         if (p->plan) rocfft_plan_destroy(p->plan);
+        if (p->tail) rocfft_plan_destroy(p->tail);
         delete p;
         return OFS_EFFT;
     }
+    if (wb > p->work_bytes) p->work_bytes = wb;
     p->precision = precision;
     p->N = N;
     p->n_windows = n_windows;
@@ -205,6 +224,7 @@ int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows,
             if (p->cb_dev) hipFree(p->cb_dev);
             if (p->cb_host) hipHostFree(p->cb_host);
             rocfft_plan_destroy(p->plan);
+            if (p->tail) rocfft_plan_destroy(p->tail);
             delete p;
             return OFS_EHIP;
         }
@@ -214,10 +234,16 @@ int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows,
     return OFS_OK;
 }
 
+int64_t ofs_zc_fft_plan_chunk(const void* plan) {
+    const ZcFftPlan* p = static_cast<const ZcFftPlan*>(plan);
+    return p ? p->chunk : 0;
+}
+
 int32_t ofs_zc_fft_plan_destroy(void* plan) {
     ZcFftPlan* p = static_cast<ZcFftPlan*>(plan);
     if (!p) return OFS_OK;
     if (p->plan) rocfft_plan_destroy(p->plan);
+    if (p->tail) rocfft_plan_destroy(p->tail);
     if (p->cb_dev) hipFree(p->cb_dev);
     if (p->cb_host) hipHostFree(p->cb_host);
     delete p;
@@ -289,17 +315,29 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
     }
     const size_t esz = p->precision == OFS_FP32 ? 8 : 16;
     const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
+    if (p->chunk % n_br) { rocfft_execution_info_destroy(info); return OFS_EINVAL; }
+    const int64_t cs = p->chunk / n_br;             // streams per rocFFT execution
     int32_t rc = OFS_OK;
-    for (int64_t off = 0; off < n_off && s == rocfft_status_success; ++off) {
-        // windows x[b][br][off+cp : off+cp+N], distance T: one batched transform per offset
-        void* in[1] = {const_cast<char*>(static_cast<const char*>(x)) + (size_t)(off + cp) * esz};
-        void* out[1] = {spectrum};
-        s = rocfft_execute(p->plan, in, out, info);
-        if (s != rocfft_status_success) break;
-        g.off = off;
-        if (p->precision == OFS_FP32) hipLaunchKernelGGL(zc_gather_kernel<float>, dim3(grid), dim3(ZWG), 0, st, g);
-        else hipLaunchKernelGGL(zc_gather_kernel<double>, dim3(grid), dim3(ZWG), 0, st, g);
-        if (hipGetLastError() != hipSuccess) { rc = OFS_EHIP; break; }
+    // windows x[b][br][off+cp : off+cp+N], distance T: one batched transform per chunk of streams
+    // and offset.  A chunked plan reuses one [chunk][N] spectrum buffer small enough to stay in the
+    // Infinity Cache between the FFT's store and the gather's read, and walks a chunk's offsets
+    // back to back so its input windows are re-read from cache too.
+    for (int64_t b0 = 0; b0 < B && s == rocfft_status_success && rc == OFS_OK; b0 += cs) {
+        const int64_t nb = B - b0 < cs ? B - b0 : cs;
+        const unsigned gc = (unsigned)((nb + ZWG / 64 - 1) / (ZWG / 64));
+        g.b0 = b0;
+        g.B = nb;
+        for (int64_t off = 0; off < n_off; ++off) {
+            void* in[1] = {const_cast<char*>(static_cast<const char*>(x)) +
+                           ((size_t)b0 * n_br * T + (size_t)(off + cp)) * esz};
+            void* out[1] = {spectrum};
+            s = rocfft_execute(nb == cs ? p->plan : p->tail, in, out, info);
+            if (s != rocfft_status_success) break;
+            g.off = off;
+            if (p->precision == OFS_FP32) hipLaunchKernelGGL(zc_gather_kernel<float>, dim3(gc), dim3(ZWG), 0, st, g);
+            else hipLaunchKernelGGL(zc_gather_kernel<double>, dim3(gc), dim3(ZWG), 0, st, g);
+            if (hipGetLastError() != hipSuccess) { rc = OFS_EHIP; break; }
+        }
     }
     rocfft_execution_info_destroy(info);
     if (s != rocfft_status_success) return OFS_EFFT;

@@ -95,18 +95,21 @@ def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, te
 class FFTPlan:
     """Caller-owned rocFFT plan for ``n_windows`` windows of ``N`` samples at distance ``T``.
     ``prune_bins`` > 0: pruned output (rocFFT store callback keeps only the template bins; the
-    spectrum buffer is then [n_windows][prune_bins])."""
+    spectrum buffer is then [chunk][prune_bins]).  ``chunk`` windows per rocFFT execution (0: all
+    of them); ``self.chunk`` is the spectrum buffer's row count."""
 
-    def __init__(self, precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0):
+    def __init__(self, precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0):
         import ctypes
         self._lib = _lib.lib()
         h = ctypes.c_void_p()
         wb = ctypes.c_size_t()
-        _lib.check(self._lib.ofs_zc_fft_plan_create2(int(precision), int(N), int(n_windows), int(T), int(prune_bins),
-                                                    ctypes.byref(h), ctypes.byref(wb)), "ofs_zc_fft_plan_create2")
+        _lib.check(self._lib.ofs_zc_fft_plan_create3(int(precision), int(N), int(n_windows), int(T), int(prune_bins),
+                                                    int(chunk), ctypes.byref(h), ctypes.byref(wb)),
+                   "ofs_zc_fft_plan_create3")
         self.handle, self.work_bytes = h.value, int(wb.value)
         self.prune_bins = int(prune_bins)
-        self.key = (int(precision), int(N), int(n_windows), int(T), int(prune_bins))
+        self.chunk = int(self._lib.ofs_zc_fft_plan_chunk(self.handle))
+        self.key = (int(precision), int(N), int(n_windows), int(T), int(prune_bins), int(chunk))
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
@@ -117,19 +120,30 @@ class FFTPlan:
 _plans: dict = {}
 
 
-def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0) -> FFTPlan:
-    key = (precision, N, n_windows, T, prune_bins)
+def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0) -> FFTPlan:
+    key = (precision, N, n_windows, T, prune_bins, chunk)
     p = _plans.get(key)
     if p is None:
         if len(_plans) >= 8:
             _plans.clear()
-        p = _plans[key] = FFTPlan(precision, N, n_windows, T, prune_bins)
+        p = _plans[key] = FFTPlan(precision, N, n_windows, T, prune_bins, chunk)
     return p
+
+
+def default_chunk(n_windows: int, n_br: int, N: int, esz: int) -> int:
+    """Windows per rocFFT execution for the dense leg: a spectrum buffer of about CHUNK_BYTES
+    (a multiple of n_br), so it stays in the 256 MiB Infinity Cache between the FFT and the gather."""
+    per = max(n_br, (CHUNK_BYTES // (N * esz)) // n_br * n_br)
+    return 0 if per >= n_windows else per
+
+
+CHUNK_BYTES = 64 << 20
 
 
 def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                             N: int | None = None, cp: int | None = None, *,
-                                            return_peak: bool = False, pruned: bool = False):
+                                            return_peak: bool = False, pruned: bool = False,
+                                            chunk: int | None = None):
     """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
     batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
     complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
@@ -137,7 +151,9 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     ``pruned`` (N a power of two <= 4096, distinct bins): rocFFT's store callback keeps only the
     template bins, so no dense spectrum is written (1.03x the algorithmic bytes instead of 2.02x);
     measured 2.3x SLOWER on cfg5 (34.2 vs 15.0 ms: rocFFT's callback kernel calls the store
-    through a function pointer per element), hence off by default."""
+    through a function pointer per element), hence off by default.
+    ``chunk``: windows per rocFFT execution (None: ``default_chunk``; 0: one execution over the
+    whole batch); the spectrum scratch is [chunk][N]."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -161,8 +177,13 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
                     torch.empty((0,), dtype=torch.float64, device=dev))
         return out
     pruned = bool(pruned) and N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
-    plan = _plan(prec, N, batch.B * batch.nb, batch.T, int(idx.size) if pruned else 0)
-    spec = torch.empty((batch.B * batch.nb, int(idx.size) if pruned else N), dtype=batch.data.dtype, device=dev)
+    nw = batch.B * batch.nb
+    if chunk is None:
+        chunk = 0 if pruned else default_chunk(nw, batch.nb, N, batch.data.element_size())
+    if chunk and chunk % batch.nb:
+        raise ValueError("chunk must be a multiple of the branch count")
+    plan = _plan(prec, N, nw, batch.T, int(idx.size) if pruned else 0, int(chunk))
+    spec = torch.empty((plan.chunk, int(idx.size) if pruned else N), dtype=batch.data.dtype, device=dev)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
     out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
     pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None

@@ -22,7 +22,7 @@ def lib():
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int32_t|const char\*)\s+(ofs_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(ofs_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_the_boundary():

@@ -136,3 +136,37 @@ def test_pruned_store_callback_equals_dense(prec, N, cp, T, nb):
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=tol, atol=tol * 1e-3)
     ref = np.stack([O.zc_freq_metric(x[k], N, cp, idx, t, e) for k in range(B)])
     np.testing.assert_allclose(a.cpu().numpy(), ref, rtol=1e-9 if prec == "c128" else 2e-5, atol=1e-7 if prec == "c128" else 2e-5)
+
+
+@pytest.mark.parametrize("prec,nb,chunk,pruned", [("c128", 1, 7, False), ("c128", 2, 6, False), ("c64", 3, 9, False),
+                                                  ("c64", 2, 4, True), ("c64", 1, 64, False)])
+def test_rocfft_chunked_equals_one_execution(prec, nb, chunk, pruned):
+    """Chunked plans (ofs_zc_fft_plan_create3: rocFFT executions over `chunk` windows into one
+    reused spectrum buffer, chunk not dividing the batch -> a tail plan) give the one-execution
+    result, several offsets per stream; fp64 also against the oracle."""
+    N, cp, T, B = 256, 32, 300, 23
+    rng = np.random.default_rng(chunk * 7 + nb)
+    x = rng_c(rng, B, nb, T)
+    x[3, :, cp + 5:cp + 5 + N] += 3 * O.pss_symbol(N)
+    x = x.astype(np.complex128 if prec == "c128" else np.complex64)
+    idx, t, e = O.zc_template()
+    xd = torch.from_numpy(x).cuda()
+    m0, pk0, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                                 pruned=pruned, chunk=0)
+    m1, pk1, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                                 pruned=pruned, chunk=chunk)
+    a0, a1 = m0.cpu().numpy(), m1.cpu().numpy()
+    tol = dict(rtol=1e-9, atol=1e-11) if prec == "c128" else dict(rtol=0, atol=2e-5)
+    np.testing.assert_allclose(a1, a0, **tol)
+    if prec == "c128":
+        assert torch.equal(pk0, pk1)
+        for b in (0, 3, B - 1):
+            np.testing.assert_allclose(a1[b], O.zc_freq_metric(x[b], N, cp, idx, t, e), **tol)
+    assert int(pk1[3]) == 5
+
+
+def test_rocfft_chunk_must_split_branches():
+    idx, t, e = O.zc_template()
+    with pytest.raises(ValueError):
+        zc_freq.compute_frequency_metric_rocfft_batched(torch.ones((4, 2, 80), dtype=torch.complex64).cuda(),
+                                                        idx, t, e, N=64, cp=16, chunk=3)

@@ -314,7 +314,7 @@ def cfg3_fp64(dev, st, steps, warmup):
                 bytes_per_sample="16 in + P 16 + R 8 + M 8")
 
 
-def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5, pruned=None):
+def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5, pruned=None, chunked=False):
     """cfg5 through the rocFFT leg (ofs_zc_freq_metric_fft: batched rocFFT of every window into a
     dense spectrum, then the HIP gather/metric kernel and the per-sequence argmax), same input as
     cfg5.  alg_bytes counts the same 8 B/sample + output as cfg5 so Msamples/s and frac compare
@@ -331,16 +331,22 @@ def cfg5_rocfft(dev, st, steps, warmup, n_seq=1 << 20, seed=5, pruned=None):
     idx32 = np.ascontiguousarray(idx.astype(np.int32))
     tb = np.ascontiguousarray(t.astype(np.complex128))
     nb_ = len(idx32)
-    spec = torch.empty((n_seq, nb_ if pruned else N), dtype=torch.complex64, device=dev)
+    chunk = 0
+    if chunked:
+        chunk = int(os.environ.get("OFS_ZC_FFT_CHUNK", "0")) or zc_freq.default_chunk(n_seq, 1, N, 8)
+    plan = zc_freq.FFTPlan(_lib.FP32, N, n_seq, N, nb_ if pruned else 0, min(chunk, n_seq))
+    spec = torch.empty((plan.chunk, nb_ if pruned else N), dtype=torch.complex64, device=dev)
     out = torch.empty((n_seq, 1), dtype=torch.float32, device=dev)
     pk = torch.empty((n_seq,), dtype=torch.int64, device=dev)
-    plan = zc_freq.FFTPlan(_lib.FP32, N, n_seq, N, nb_ if pruned else 0)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
     L_ = _lib.lib()
     args = (plan.handle, _lib.C64, x.data_ptr(), n_seq, 1, N, N, 0, 62, idx32.ctypes.data, tb.ctypes.data, e,
             spec.data_ptr(), _lib.ptr(work), out.data_ptr(), pk.data_ptr(), None, st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_zc_freq_metric_fft(*args), "zc_freq rocfft"), steps, warmup, st)
-    return dict(config="cfg5_rocfft" if pruned else "cfg5_rocfft_dense",
+    name = "cfg5_rocfft" if pruned else "cfg5_rocfft_dense"
+    if chunked:
+        name = ("cfg5_rocfft_pruned_chunked" if pruned else "cfg5_rocfft_chunked")
+    return dict(config=name, chunk_windows=plan.chunk,
                 workload=f"zc_freq 62-bin metric via rocFFT, N={N}, cp=0, {n_seq} sequences x {N} c64",
                 kernel=("rocFFT fp32 C2C + pruning store callback (template bins only) + zc_gather_kernel + "
                         "row_argmax_kernel" if pruned else
@@ -534,6 +540,7 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
            "zc_detect_state": lambda *a, **k: zc_detect(*a, state=True, **k),
            "zc_detect_seq": lambda *a, **k: zc_detect(*a, seq=True, **k),
            "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
+           "cfg5_rocfft_chunked": lambda *a, **k: cfg5_rocfft(*a, pruned=False, chunked=True, **k),
            "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
@@ -541,7 +548,7 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
 
 # strong-scaled configs: global batch and the keyword that receives the rank's shard
 SHARDED = {"cfg4": ("cfg4_global", "B"), "cfg5": ("cfg5_global", "n_seq"), "cfg5_rocfft": ("cfg5_global", "n_seq"),
-           "cfg5_rocfft_dense": ("cfg5_global", "n_seq")}
+           "cfg5_rocfft_dense": ("cfg5_global", "n_seq"), "cfg5_rocfft_chunked": ("cfg5_global", "n_seq")}
 
 
 def main(argv=None):
