@@ -335,7 +335,36 @@ __device__ __forceinline__ bool same_bits(double a, double b) {
     return __double_as_longlong(a) == __double_as_longlong(b);
 }
 
-template <int E, int MW, int CPNA>
+// One walker lane's pass over a segment (phase B below): the reference's IIR (minn_rtl.py:706-715)
+// exactly as written, branch-free per sample, SM = 0 float s += (c - s)/2^k, 1 shift 0 (s = c),
+// 2 RTL floor shift; the threshold decision (:717-722) goes into the stored value's sign bit.
+template <int SM>
+__device__ __forceinline__ void rtl_walk(const double* __restrict__ wcp, double* __restrict__ wes, int n, int v0,
+                                         double inv, double scale, int shift, double& sv, long long& siv) {
+    constexpr long long SIGN = (long long)(1ull << 63);
+    auto step = [&](double c, double es) -> double {
+        if constexpr (SM == 0) sv = sv + (c - sv) * inv;
+        else if constexpr (SM == 1) sv = c;
+        else {
+            const long long ci = (long long)c;
+            siv = shift == 0 ? ci : siv + ((ci - siv) >> shift);
+            sv = (double)siv;
+        }
+        return __longlong_as_double(__double_as_longlong(sv) | (sv * scale >= es ? SIGN : 0ll));
+    };
+    int li = 0;
+    for (; li < v0; ++li) wes[seg_at(li)] = sv;                  // before metric_valid: state held
+    for (; li + 8 <= n; li += 8) {
+        double cb[8], eb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { cb[u] = wcp[seg_at(li + u)]; eb[u] = wes[seg_at(li + u)]; }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wes[seg_at(li + u)] = step(cb[u], eb[u]);
+    }
+    for (; li < n; ++li) wes[seg_at(li)] = step(wcp[seg_at(li)], wes[seg_at(li)]);
+}
+
+template <int E, int MW, int CPNA, int NBM>
 __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #pragma clang fp contract(off)
     constexpr int RL = 64 * E;
@@ -347,10 +376,18 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const int w = threadIdx.x >> 6;
     const int wpb = blockDim.x >> 6;
     const int64_t b = (int64_t)blockIdx.x * wpb + w;
-    if (b >= a.B) return;
     const int64_t T = a.T;
     const int nb_ = a.nb;
-    double* hae_ = rsm + (rtl_wave_lds(E, MW, nb_) / sizeof(double)) * w;
+    const bool seq = a.smooth || a.corr_scaled || a.above || a.detect;
+    const size_t wave_dbl = rtl_wave_lds(E, MW, nb_) / sizeof(double);
+    const int smode = a.smooth_mode == 1 ? 2 : (a.shift == 0 ? 1 : 0);
+    const bool walk = seq && smode == 2;        // the RTL floor IIR runs in a walker lane (barriers)
+    if (b >= a.B) {                 // no stream: still meet the workgroup's two barriers per segment
+        if (walk)
+            for (int64_t g = 0; g < (T + SEG - 1) / SEG; ++g) { __syncthreads(); __syncthreads(); }
+        return;
+    }
+    double* hae_ = rsm + wave_dbl * w;
     double* hac_ = hae_ + NR * E * 64;
     double* hcp = hac_ + NR * E * 64;                                // segment corr_positive
     double* hes = hcp + SEG_PAD;                                     // segment energy_scaled
@@ -378,8 +415,6 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const double inv = ldexp(1.0, -(a.shift > 0 ? a.shift : 0));   // exact 1 / 2^shift
     const double keep = 1.0 - inv;
     const double scale = (double)(1ll << a.frac_bits);
-    const bool seq = a.smooth || a.corr_scaled || a.above || a.detect;
-    const int smode = a.smooth_mode == 1 ? 2 : (a.shift == 0 ? 1 : 0);
     double CC = 0.0, CE = 0.0;
     double sm = 0.0;                                               // IIR state carried between segments
     long long si = 0;
@@ -390,7 +425,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 
     // rows stream in PD rows ahead of use (register queue shifted by one row per step)
     constexpr int PD = E == 1 ? 8 : (E == 2 ? 4 : 2);
-    constexpr int NBM = 4;                                         // branches supported
+    // NBM: branches held per row (1, or 4 = the most supported; CPNA > 0: CPNA)
     int32_t nx[PD][NBM][E];
     // one row of every branch (CPNA > 0: packed 12-bit words, CPNA branches)
     auto load_row = [&](int64_t n0, int32_t (&dst)[NBM][E]) {
@@ -491,50 +526,50 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             CC += qc.tot; CE += qe.tot;
         }
         if (!seq) continue;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-        // ---------------- phase B: smoothing of the segment, lane j = chunk j ----------------
         const int64_t c0 = s0 + (int64_t)SC * lane;                   // first sample of my chunk
         const int64_t send = min(T, s0 + SEG);
-        double own[SC];                                                // smoothed, my chunk
-        int fail_from = 64;                                            // first chunk to redo serially
-        if (smode == 1) {                                              // shift 0: s = c (no chain)
+        bool abv[SC];
+        double cp8[SC], own[SC];
+        if (walk) {
+            // ---------- phase B (RTL floor mode): one walker lane per stream of the workgroup -----
+            // The integer floor-shift recursion does not merge nearby trajectories, so it runs as
+            // written: wave 0, lane t walking stream t through the segment's corr_positive /
+            // energy_scaled in LDS (rtl_walk).  The smoothed value goes back over energy_scaled
+            // with the threshold decision in its sign bit (the state is never negative).
+            __syncthreads();
+            if (w == 0 && lane < wpb && (int64_t)blockIdx.x * wpb + lane < a.B) {
+                const double* wcp = rsm + wave_dbl * lane + 2 * NR * E * 64;
+                double* wes = const_cast<double*>(wcp) + SEG_PAD;
+                const int n = (int)(send - s0);
+                const int v0 = (int)max((int64_t)0, min((int64_t)n, (int64_t)vstart - s0));
+                rtl_walk<2>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
+            }
+            __syncthreads();
 #pragma unroll
             for (int e = 0; e < SC; ++e) {
                 const int64_t p = c0 + e;
-                own[e] = (p >= vstart && p < T) ? hcp[seg_at(SC * lane + e)] : 0.0;
+                const int at = seg_at(SC * lane + e);
+                cp8[e] = hcp[at];
+                const long long v = __double_as_longlong(hes[at]);
+                own[e] = __longlong_as_double(v & 0x7fffffffffffffffll);
+                abv[e] = p < T && v < 0;
             }
-            // state holds where invalid (before vstart: the initial 0); positions >= T unused
-            if (send - 1 >= vstart) sm = hcp[seg_at((int)(send - 1 - s0))];
-        } else if (smode == 0) {
-            // 1. chunk maps from s = 0: s_out = A·s_in + Z (approximate arithmetic is fine here)
-            double A = 1.0, Z = 0.0;
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // ---------- phase B (float IIR): segment-parallel, lane j = chunk j -----------------
+            if (smode == 1) {                                          // shift 0: s = c (no chain)
 #pragma unroll
-            for (int e = 0; e < SC; ++e) {
-                const int64_t p = c0 + e;
-                if (p >= vstart && p < T) {
-                    const double c = hcp[seg_at(SC * lane + e)];
-                    Z = Z + (c - Z) * inv;
-                    A = A * keep;
+                for (int e = 0; e < SC; ++e) {
+                    const int64_t p = c0 + e;
+                    own[e] = (p >= vstart && p < T) ? hcp[seg_at(SC * lane + e)] : 0.0;
                 }
-            }
-            // inclusive wave scan of the affine maps (compose lane-1's map first, then mine)
-            {
-                double sa = A, sz = Z;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const double pa = __shfl_up(sa, d, 64), pz = __shfl_up(sz, d, 64);
-                    if (lane >= d) { sz = sa * pz + sz; sa = sa * pa; }
-                }
-                // entering state of my chunk: exclusive map applied to the carried exact state
-                const double ea = __shfl_up(sa, 1, 64), ez = __shfl_up(sz, 1, 64);
-                double enter = lane == 0 ? sm : ea * sm + ez;
-                // 2./3. exact chunk runs until the chain is self-consistent: every lane runs the
-                // reference recursion over its chunk from `enter`, then takes lane-1's leaving
-                // state as its new `enter`; stop when no lane's entering state changes.  Lane 0
-                // starts exact, and after round r lanes 0..r are exact, so <= 64 rounds.
+                // state holds where invalid (before vstart: the initial 0); positions >= T unused
+                if (send - 1 >= vstart) sm = hcp[seg_at((int)(send - 1 - s0))];
+            } else {
+                // 1. chunk maps from s = 0: s_out = A·s_in + Z (approximate arithmetic is fine here)
+                double A = 1.0, Z = 0.0;
                 double cv[SC];
                 bool upd[SC];
 #pragma unroll
@@ -542,68 +577,59 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                     const int64_t p = c0 + e;
                     upd[e] = p >= vstart && p < T;
                     cv[e] = hcp[seg_at(SC * lane + e)];
+                    if (upd[e]) {
+                        Z = Z + (cv[e] - Z) * inv;
+                        A = A * keep;
+                    }
                 }
-                int round = 0;
-                for (; round <= 64; ++round) {
+                // inclusive wave scan of the affine maps (lane-1's map first, then mine): DPP
+                // ladder row_shr 1/2/4/8, row_bcast 15/31
+                double sa = A, sz = Z;
+                const int rl = lane & 15;
+                auto comb = [&](double pa, double pz, bool take) {
+                    if (take) { sz = sa * pz + sz; sa = sa * pa; }
+                };
+                { const double pa = ofs::dpp_d<0x111>(sa), pz = ofs::dpp_d<0x111>(sz); comb(pa, pz, rl >= 1); }
+                { const double pa = ofs::dpp_d<0x112>(sa), pz = ofs::dpp_d<0x112>(sz); comb(pa, pz, rl >= 2); }
+                { const double pa = ofs::dpp_d<0x114>(sa), pz = ofs::dpp_d<0x114>(sz); comb(pa, pz, rl >= 4); }
+                { const double pa = ofs::dpp_d<0x118>(sa), pz = ofs::dpp_d<0x118>(sz); comb(pa, pz, rl >= 8); }
+                { const double pa = ofs::dpp_d<0x142>(sa), pz = ofs::dpp_d<0x142>(sz); comb(pa, pz, (lane & 31) >= 16); }
+                { const double pa = ofs::dpp_d<0x143>(sa), pz = ofs::dpp_d<0x143>(sz); comb(pa, pz, lane >= 32); }
+                // entering state of my chunk: exclusive map applied to the carried exact state
+                const double ea = ofs::wave_shr1(sa, lane, 1.0), ez = ofs::wave_shr1(sz, lane, 0.0);
+                double enter = lane == 0 ? sm : ea * sm + ez;
+                // 2./3. exact chunk runs until the chain is self-consistent: every lane runs the
+                // reference recursion over its chunk from `enter`, then takes lane-1's leaving
+                // state (DPP wave_shr:1) as its new `enter`; stop when no lane's entering state
+                // changes.  Lane 0 starts exact, and after round r lanes 0..r are exact: <= 64 rounds.
+                for (int round = 0; round <= 64; ++round) {
                     double st = enter;
 #pragma unroll
                     for (int e = 0; e < SC; ++e) {
                         if (upd[e]) st = st + (cv[e] - st) * inv;
                         own[e] = st;
                     }
-                    const double up = __shfl_up(st, 1, 64);
-                    const double prev_leave = lane == 0 ? sm : up;
-                    const bool ok = same_bits(enter, prev_leave);
-                    if (__ballot(!ok) == 0) {
+                    const double prev_leave = ofs::wave_shr1(st, lane, sm);
+                    if (__ballot(!same_bits(enter, prev_leave)) == 0) {
                         sm = readlane(st, 63);
                         break;
                     }
                     enter = prev_leave;
                 }
-#ifdef OFS_RTL_DEBUG
-                if (b < 4 && lane == 0) printf("rtl b=%ld seg=%d rounds=%d\n", (long)b, g, round);
-#endif
             }
-        } else {
-            fail_from = 0;
-        }
-#ifdef OFS_RTL_DEBUG
-        if (b < 4 && lane == 0) printf("rtl b=%ld seg=%d fail_from=%d shift=%d smode=%d\n", (long)b, g, fail_from,
-                                       a.shift, smode);
-#endif
-        if (fail_from < 64) {
-            // sequential recomputation from chunk fail_from with the exact state (wave-uniform)
-            double sv = fail_from == 0 ? sm : readlane(own[SC - 1], fail_from - 1);
-            long long siv = si;
-            for (int q = fail_from; q < 64; ++q) {
+            // ---------- phase C: threshold (chunk layout) -----------------------------------------
 #pragma unroll
-                for (int e = 0; e < SC; ++e) {
-                    const int64_t p = s0 + (int64_t)SC * q + e;
-                    if (p >= vstart && p < T) {
-                        const double c = hcp[seg_at(SC * q + e)];
-                        if (smode == 0) {
-                            sv = sv + (c - sv) * inv;
-                        } else {                                       // RTL floor shift
-                            const long long ci = (long long)c;
-                            siv = (a.shift == 0) ? ci : siv + ((ci - siv) >> a.shift);
-                            sv = (double)siv;
-                        }
-                    }
-                    if (lane == q) own[e] = sv;
-                }
+            for (int e = 0; e < SC; ++e) {
+                const int64_t p = c0 + e;
+                const int at = seg_at(SC * lane + e);
+                cp8[e] = hcp[at];
+                abv[e] = p >= vstart && p < T && (own[e] * scale >= hes[at]);      // minn_rtl.py:717-722
             }
-            sm = sv; si = siv;
         }
-
-        // ---------------- phase C: threshold, gate, stores (chunk layout) ----------------------
-        bool abv[SC];
-        double cp8[SC];
+        // ---------- phase C: gate and stores -----------------------------------------------------
 #pragma unroll
         for (int e = 0; e < SC; ++e) {
             const int64_t p = c0 + e;
-            const int at = seg_at(SC * lane + e);
-            cp8[e] = hcp[at];
-            abv[e] = p >= vstart && p < T && (own[e] * scale >= hes[at]);      // minn_rtl.py:717-722
             if (p < T) {
                 const int64_t gi = row_off + p;
                 if (a.smooth) a.smooth[gi] = own[e];
@@ -657,7 +683,7 @@ int aa_launch_mr(int fmt, int mr, int na, const AaFastArgs& a, hipStream_t st) {
     return 0;
 }
 
-template <int E, int MW, int CPNA>
+template <int E, int MW, int CPNA, int NBM>
 int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
     const size_t per_wave = rtl_wave_lds(E, MW, a.nb);
     int wpb = 4;                                             // waves (streams) per workgroup
@@ -665,7 +691,7 @@ int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
     if (ev && (atoi(ev) == 1 || atoi(ev) == 2)) wpb = atoi(ev);
     while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
     const size_t lds = per_wave * wpb;
-    auto k = rtl_exact_kernel<E, MW, CPNA>;
+    auto k = rtl_exact_kernel<E, MW, CPNA, NBM>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return OFS_EHIP;
@@ -675,8 +701,8 @@ int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
 
 template <int E, int MW>
 int rtl_launch(int fmt, const RtlExactArgs& a, hipStream_t st) {
-    if (fmt == OFS_CP12) return a.nb == 1 ? rtl_launch_k<E, MW, 1>(a, st) : rtl_launch_k<E, MW, 2>(a, st);
-    return rtl_launch_k<E, MW, 0>(a, st);
+    if (fmt == OFS_CP12) return a.nb == 1 ? rtl_launch_k<E, MW, 1, 1>(a, st) : rtl_launch_k<E, MW, 2, 2>(a, st);
+    return a.nb == 1 ? rtl_launch_k<E, MW, 0, 1>(a, st) : rtl_launch_k<E, MW, 0, 4>(a, st);
 }
 
 }  // namespace

@@ -151,6 +151,33 @@ __global__ __launch_bounds__(ZWG) void row_argmax_kernel(const R* __restrict__ v
     }
 }
 
+// Short rows (n <= 32, e.g. one offset per sequence on cfg5): one thread per row, same semantics.
+template <class R>
+__global__ __launch_bounds__(ZWG) void row_argmax_short_kernel(const R* __restrict__ v, int64_t B, int32_t n,
+                                                              int64_t* __restrict__ idx, double* __restrict__ val) {
+    const int64_t b = (int64_t)blockIdx.x * ZWG + threadIdx.x;
+    if (b >= B) return;
+    const R* row = v + b * n;
+    double best = (double)row[0];
+    int64_t bi = 0;
+    for (int j = 1; j < n && best == best; ++j) {       // stop at the first NaN (it wins)
+        const double x = (double)row[j];
+        if (x != x || x > best) { best = x; bi = j; }
+    }
+    if (idx) idx[b] = bi;
+    if (val) val[b] = best;
+}
+
+template <class R>
+void launch_argmax(const R* v, int64_t B, int64_t n, int64_t* idx, double* val, hipStream_t st) {
+    if (n <= 32)
+        hipLaunchKernelGGL(row_argmax_short_kernel<R>, dim3((unsigned)((B + ZWG - 1) / ZWG)), dim3(ZWG), 0, st, v, B,
+                           (int32_t)n, idx, val);
+    else
+        hipLaunchKernelGGL(row_argmax_kernel<R>, dim3((unsigned)((B + ZWG / 64 - 1) / (ZWG / 64))), dim3(ZWG), 0, st,
+                           v, B, n, idx, val);
+}
+
 std::once_flag g_setup;
 
 }  // namespace
@@ -344,11 +371,9 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
     if (rc) return rc;
     if (peak_index || peak_value) {
         if (p->precision == OFS_FP32)
-            hipLaunchKernelGGL(row_argmax_kernel<float>, dim3(grid), dim3(ZWG), 0, st,
-                               static_cast<const float*>(metric), B, n_off, peak_index, peak_value);
+            launch_argmax(static_cast<const float*>(metric), B, n_off, peak_index, peak_value, st);
         else
-            hipLaunchKernelGGL(row_argmax_kernel<double>, dim3(grid), dim3(ZWG), 0, st,
-                               static_cast<const double*>(metric), B, n_off, peak_index, peak_value);
+            launch_argmax(static_cast<const double*>(metric), B, n_off, peak_index, peak_value, st);
         if (hipGetLastError() != hipSuccess) return OFS_EHIP;
     }
     return OFS_OK;
@@ -359,14 +384,9 @@ int32_t ofs_row_argmax(int32_t precision, const void* v, int64_t B, int64_t n, i
     if ((precision != OFS_FP32 && precision != OFS_FP64) || !v || B < 0 || n < 1 || (!index && !value))
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
-    const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (precision == OFS_FP32)
-        hipLaunchKernelGGL(row_argmax_kernel<float>, dim3(grid), dim3(ZWG), 0, st, static_cast<const float*>(v), B, n,
-                           index, value);
-    else
-        hipLaunchKernelGGL(row_argmax_kernel<double>, dim3(grid), dim3(ZWG), 0, st, static_cast<const double*>(v), B,
-                           n, index, value);
+    if (precision == OFS_FP32) launch_argmax(static_cast<const float*>(v), B, n, index, value, st);
+    else launch_argmax(static_cast<const double*>(v), B, n, index, value, st);
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
 

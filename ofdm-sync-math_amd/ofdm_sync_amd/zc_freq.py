@@ -152,8 +152,10 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     template bins, so no dense spectrum is written (1.03x the algorithmic bytes instead of 2.02x);
     measured 2.3x SLOWER on cfg5 (34.2 vs 15.0 ms: rocFFT's callback kernel calls the store
     through a function pointer per element), hence off by default.
-    ``chunk``: windows per rocFFT execution (None: ``default_chunk``; 0: one execution over the
-    whole batch); the spectrum scratch is [chunk][N]."""
+    ``chunk``: windows per rocFFT execution (None or 0: one execution over the whole batch;
+    ``default_chunk`` sizes one for the Infinity Cache); the spectrum scratch is [chunk][N].  Chunking
+    keeps the spectrum round trip on-die but measured neutral on cfg5 (17.5 vs 17.7 ms): rocFFT's
+    own 4096-point kernel, not HBM, bounds the leg."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -179,7 +181,7 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     pruned = bool(pruned) and N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
     nw = batch.B * batch.nb
     if chunk is None:
-        chunk = 0 if pruned else default_chunk(nw, batch.nb, N, batch.data.element_size())
+        chunk = 0                                       # one execution (chunking measured neutral)
     if chunk and chunk % batch.nb:
         raise ValueError("chunk must be a multiple of the branch count")
     plan = _plan(prec, N, nw, batch.T, int(idx.size) if pruned else 0, int(chunk))

@@ -100,14 +100,17 @@ def test_rocfft_too_short_and_bad_input():
                                                         idx, t, e, N=64, cp=16)
 
 
+@pytest.mark.parametrize("n", [1000, 33, 32, 7])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-def test_row_argmax_numpy_semantics(dtype):
+def test_row_argmax_numpy_semantics(dtype, n):
+    """Wave-per-row kernel (n > 32) and thread-per-row kernel (n <= 32): numpy's first argmax."""
     rng = np.random.default_rng(7)
-    v = rng.integers(0, 5, size=(37, 1000)).astype(np.float64)    # many ties: first index must win
+    v = rng.integers(0, 5, size=(300, n)).astype(np.float64)     # many ties: first index must win
     v[3, :] = -np.inf
-    v[4, 500] = np.nan
-    v[4, 900] = np.nan
-    v[5, 999] = 100.0
+    v[4, n // 2] = np.nan
+    v[4, n - 1] = np.nan
+    v[8, 0] = np.nan
+    v[5, n - 1] = 100.0
     v[6, 0] = 100.0
     v[7, :] = 1.0
     idx, val = zc_freq.peak_index_batched(torch.from_numpy(v).to(dtype).cuda())

@@ -6,19 +6,14 @@ Writes build/libofdmsync_<name>.so (source-hash check is skipped for OFS_LIB bui
 """
 import concurrent.futures as cf
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "ofdm-sync-math_amd", "csrc")
+sys.path.insert(0, ROOT)
+import __graft_entry__ as G  # noqa: E402
+
+CSRC = G.CSRC
 OUT = os.path.join(ROOT, "build")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.join(ROOT, "include")]
-LIBS = ["-L/opt/rocm/lib", "-lrocfft", "-Wl,-rpath,/opt/rocm/lib"]
-
-
-def cc(src, obj, extra):
-    subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *extra, "-c", src, "-o", obj], check=True)
-    return obj
 
 
 def main():
@@ -26,16 +21,15 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(f for f in os.listdir(CSRC) if f.endswith(".hip"))
     with cf.ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
-        base = {s: ex.submit(cc, os.path.join(CSRC, s), os.path.join(OUT, s + ".o"), []) for s in srcs if s != tu}
+        base = [ex.submit(G.compile_cached, os.path.join(CSRC, s)) for s in srcs if s != tu]
         var = {}
         for v in variants:
             name, _, fl = v.partition("=")
-            var[name] = ex.submit(cc, os.path.join(CSRC, tu), os.path.join(OUT, f"{tu}.{name}.o"), fl.split())
-        objs = [f.result() for f in base.values()]
+            var[name] = ex.submit(G.compile_cached, os.path.join(CSRC, tu), fl.split())
+        objs = [f.result() for f in base]
         for name, f in var.items():
             so = os.path.join(OUT, f"libofdmsync_{name}.so")
-            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so,
-                            *objs, f.result(), *LIBS], check=True)
+            G.link_lib([*objs, f.result()], so, "variant-" + name)
             print(so)
 
 
