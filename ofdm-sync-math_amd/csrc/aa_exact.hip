@@ -28,6 +28,12 @@ constexpr int XW = 256;                 // 4 waves = 4 streams per workgroup
 #ifndef OFS_XA_WG
 #define OFS_XA_WG 256
 #endif
+#ifndef OFS_XWPE1                   // min waves per SIMD of the integer L = RL kernels (tuning builds)
+#define OFS_XWPE1 1
+#endif
+#ifndef OFS_XPD1                    // their rows in flight ahead of use (tuning builds)
+#define OFS_XPD1 4
+#endif
 constexpr int XA = OFS_XA_WG;           // aa_exact_kernel workgroup (tuning builds: 64)
 
 // E consecutive int16 I/Q words (packed (I, Q) in one int32) of one lane, zero past T
@@ -149,12 +155,12 @@ struct RowPrefix {
 // valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
 // ------------------------------------------------------------------------------------------
 template <int FMT, int E, int MR, int NA>
-__global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : 1) void aa_exact_kernel(AaFastArgs a) {
+__global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : (FMT != OFS_C128 && MR == 1 && NA == 1 ? OFS_XWPE1 : 1)) void aa_exact_kernel(AaFastArgs a) {
     using X = XSamp<FMT == OFS_CP12 ? OFS_CI16 : FMT>;          // CP12 decodes to int16 I/Q words
     using W = typename X::W;
     constexpr int RL = 64 * E;
     constexpr int L = MR * RL;
-    constexpr int PD = E <= 2 ? 4 : 2;                       // rows in flight ahead of use
+    constexpr int PD = (FMT != OFS_C128 && MR == 1 && NA == 1) ? OFS_XPD1 : (E <= 2 ? 4 : 2);   // rows in flight ahead of use
     constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
     const int lane = threadIdx.x & 63;
     const int64_t b = (int64_t)xcd_block_w() * (XA / 64) + (threadIdx.x >> 6);
@@ -319,6 +325,7 @@ struct RtlExactArgs {
 #define OFS_RTL_SC 4
 #endif
 constexpr int SC = OFS_RTL_SC;
+static_assert(SC % 2 == 0, "chunk stores go out as 16-byte pairs");
 constexpr int SEG = 64 * SC;
 constexpr int SEG_PAD = SEG + SEG / SC;                // chunk stride SC + 1 doubles (banks)
 __device__ __forceinline__ int seg_at(int i) { return i + i / SC; }
@@ -411,6 +418,8 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             for (int e = 0; e < E; ++e) hx(t, m, e) = 0;
 
     const int64_t row_off = b * T;
+    const bool vec_st = (T % SC) == 0 && (reinterpret_cast<uintptr_t>(a.above) & 3) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(a.smooth) | reinterpret_cast<uintptr_t>(a.corr_scaled)) & 7) == 0;
     const int vstart = 3 * Q - 1;
     const double inv = ldexp(1.0, -(a.shift > 0 ? a.shift : 0));   // exact 1 / 2^shift
     const double keep = 1.0 - inv;
@@ -627,14 +636,34 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             }
         }
         // ---------- phase C: gate and stores -----------------------------------------------------
+        if (vec_st && c0 + SC <= T) {
+            // whole chunk (T % SC == 0, flag buffer dword-aligned): 16-byte stores, one packed flag word
+            const int64_t gi = row_off + c0;
 #pragma unroll
-        for (int e = 0; e < SC; ++e) {
-            const int64_t p = c0 + e;
-            if (p < T) {
-                const int64_t gi = row_off + p;
-                if (a.smooth) a.smooth[gi] = own[e];
-                if (a.corr_scaled) a.corr_scaled[gi] = own[e] * scale;
-                if (a.above) a.above[gi] = (uint8_t)abv[e];
+            for (int e = 0; e < SC; e += 2) {
+                if (a.smooth) *reinterpret_cast<double2*>(a.smooth + gi + e) = make_double2(own[e], own[e + 1]);
+                if (a.corr_scaled)
+                    *reinterpret_cast<double2*>(a.corr_scaled + gi + e) = make_double2(own[e] * scale, own[e + 1] * scale);
+            }
+            if (a.above) {
+                if constexpr (SC == 4) {
+                    *reinterpret_cast<uint32_t*>(a.above + gi) =
+                        (uint32_t)abv[0] | ((uint32_t)abv[1] << 8) | ((uint32_t)abv[2] << 16) | ((uint32_t)abv[3] << 24);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < SC; ++e) a.above[gi + e] = (uint8_t)abv[e];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < SC; ++e) {
+                const int64_t p = c0 + e;
+                if (p < T) {
+                    const int64_t gi = row_off + p;
+                    if (a.smooth) a.smooth[gi] = own[e];
+                    if (a.corr_scaled) a.corr_scaled[gi] = own[e] * scale;
+                    if (a.above) a.above[gi] = (uint8_t)abv[e];
+                }
             }
         }
         if (a.detect && send > vstart) {
