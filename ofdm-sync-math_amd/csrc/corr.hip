@@ -276,7 +276,12 @@ __global__ __launch_bounds__(CW) void zc_mf_kernel(ZcArgs a) {
 // registers.  fp64 throughout (the metric is a ratio of 62-bin sums).
 // ------------------------------------------------------------------------------------------
 constexpr int ZF_WAVES = 2;
-constexpr int ZF_G = 64;          // offsets per transpose group
+// offsets per transpose group: the group's [3][ZF_G][17] fp64 LDS transpose buffer sets the
+// occupancy (64: 52 KiB per 2-wave workgroup = 6 waves per CU; 16: 13 KiB, VGPR-bound instead)
+#ifndef OFS_ZF_G
+#define OFS_ZF_G 16
+#endif
+constexpr int ZF_G = OFS_ZF_G;
 struct ZfArgs {
     const void* x; int64_t B, T; int N, cp; int64_t noff, chunk, nchunks;
     int nbins; double t_energy; void* metric;
