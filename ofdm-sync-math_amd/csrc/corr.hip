@@ -275,13 +275,20 @@ __global__ __launch_bounds__(CW) void zc_mf_kernel(ZcArgs a) {
 // NB (branches, summed) is a template parameter so the per-branch window sums stay in
 // registers.  fp64 throughout (the metric is a ratio of 62-bin sums).
 // ------------------------------------------------------------------------------------------
-constexpr int ZF_WAVES = 2;
-// offsets per transpose group: the group's [3][ZF_G][17] fp64 LDS transpose buffer sets the
-// occupancy (64: 52 KiB per 2-wave workgroup = 6 waves per CU; 16: 13 KiB, VGPR-bound instead)
+// Workgroup = ZF_WAVES consecutive chunks of one stream.  When the chunk length divides N (N / chunk
+// <= ZF_NBLK blocks per window), the chunks' initial windows are sums of chunk-long BLOCK DFTs
+// B_k(m) = Σ_{j in block m} x[j] w^{kj}, and neighbouring chunks share all but one block: the
+// workgroup computes its ZF_WAVES + N/chunk - 1 blocks once (spread over its waves) and each
+// wave adds up its N/chunk of them (vs N samples per wave for a direct window).
+constexpr int ZF_WAVES = 4;
+constexpr int ZF_NBLK = 8;
+// offsets per transpose group: the [3][ZF_G][17] fp64 LDS transpose buffer per wave sets the
+// occupancy (64 with 2-wave workgroups: 52 KiB = 6 waves per CU)
 #ifndef OFS_ZF_G
 #define OFS_ZF_G 16
 #endif
 constexpr int ZF_G = OFS_ZF_G;
+constexpr int ZF_ANCHOR = 64;     // twiddle recurrence re-anchored exactly every ZF_ANCHOR offsets
 struct ZfArgs {
     const void* x; int64_t B, T; int N, cp; int64_t noff, chunk, nchunks;
     int nbins; double t_energy; void* metric;
@@ -305,14 +312,84 @@ __device__ __forceinline__ double2 twiddle(int64_t m, int N) {
     return make_double2(c, s);
 }
 
+// Σ_{j=s0}^{s0+len-1} x[j] w^{kj} for each branch (len a multiple of 64 or the tail): four
+// independent accumulator / twiddle chains (samples j = 4m + p) so the dependent FMA and twiddle
+// recurrences overlap; twiddles re-anchored exactly every 64 samples
+template <int FMT, int NB>
+__device__ __forceinline__ void zf_window(const ZfArgs& a, int64_t b, int64_t s0, int64_t len, int lane, int kb,
+                                          const double2 wk, const double2 wk4, const double2 (&wkp)[3],
+                                          double (&Wr)[NB], double (&Wi)[NB]) {
+    const int N = a.N;
+    double Pr[4][NB], Pi[4][NB];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int r = 0; r < NB; ++r) { Pr[p][r] = 0.0; Pi[p][r] = 0.0; }
+    for (int64_t j0 = s0; j0 < s0 + len; j0 += 64) {
+        const int cnt = (int)min((int64_t)64, s0 + len - j0);
+        double xr[NB], xi[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+            double2 v = make_double2(0.0, 0.0);
+            if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
+            xr[r] = v.x; xi[r] = v.y;
+        }
+        double2 tw[4];
+        tw[0] = twiddle(((int64_t)kb * j0) % N, N);                 // exact anchor per block
+#pragma unroll
+        for (int p = 1; p < 4; ++p)
+            tw[p] = make_double2(tw[0].x * wkp[p - 1].x - tw[0].y * wkp[p - 1].y,
+                                 tw[0].x * wkp[p - 1].y + tw[0].y * wkp[p - 1].x);
+        if (cnt == 64) {
+#pragma unroll 4
+            for (int u = 0; u < 64; u += 4) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                    for (int r = 0; r < NB; ++r) {
+                        const double ur = ofs::readlane(xr[r], u + p), ui = ofs::readlane(xi[r], u + p);
+                        Pr[p][r] = fma(ur, tw[p].x, fma(-ui, tw[p].y, Pr[p][r]));
+                        Pi[p][r] = fma(ur, tw[p].y, fma(ui, tw[p].x, Pi[p][r]));
+                    }
+                    const double nr = tw[p].x * wk4.x - tw[p].y * wk4.y;
+                    const double ni = tw[p].x * wk4.y + tw[p].y * wk4.x;
+                    tw[p].x = nr; tw[p].y = ni;
+                }
+            }
+        } else {
+            double2 t = tw[0];
+            for (int u = 0; u < cnt; ++u) {
+#pragma unroll
+                for (int r = 0; r < NB; ++r) {
+                    const double ur = ofs::readlane(xr[r], u), ui = ofs::readlane(xi[r], u);
+                    Pr[0][r] = fma(ur, t.x, fma(-ui, t.y, Pr[0][r]));
+                    Pi[0][r] = fma(ur, t.y, fma(ui, t.x, Pi[0][r]));
+                }
+                const double nr = t.x * wk.x - t.y * wk.y;
+                const double ni = t.x * wk.y + t.y * wk.x;
+                t.x = nr; t.y = ni;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+        Wr[r] = (Pr[0][r] + Pr[1][r]) + (Pr[2][r] + Pr[3][r]);
+        Wi[r] = (Pi[0][r] + Pi[1][r]) + (Pi[2][r] + Pi[3][r]);
+    }
+}
+
 template <int FMT, int NB>
 __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
-    __shared__ double red[ZF_WAVES][3][ZF_G][17];
+    // LDS: the per-wave transpose buffers, aliased by the workgroup's block sums before the slide
+    constexpr int RED = ZF_WAVES * 3 * ZF_G * 17;
+    constexpr int BLK = (ZF_WAVES + ZF_NBLK - 1) * NB * 64 * 2;
+    __shared__ double lds[RED > BLK ? RED : BLK];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t item = (int64_t)blockIdx.x * ZF_WAVES + wave;
-    if (item >= a.B * a.nchunks) return;              // whole wave; no block barriers below
-    const int64_t b = item / a.nchunks;
-    const int64_t o0 = (item - b * a.nchunks) * a.chunk;
+    const int64_t cgroups = (a.nchunks + ZF_WAVES - 1) / ZF_WAVES;
+    const int64_t b = blockIdx.x / cgroups;
+    const int64_t c_first = (blockIdx.x - b * cgroups) * ZF_WAVES;
+    const int64_t c = c_first + wave;                           // my chunk (may be past the end)
+    const int64_t o0 = c * a.chunk;
     const int64_t o1 = min(o0 + a.chunk, a.noff);
     const int N = a.N;
     const bool bin_live = lane < a.nbins;
@@ -320,76 +397,44 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
     const double tr = bin_live ? a.tr[lane] : 0.0, ti = bin_live ? a.ti[lane] : 0.0;
     const double emask = bin_live ? 1.0 : 0.0;
     const double2 wk = twiddle(kb, N);
-
-    double Wr[NB], Wi[NB];
-#pragma unroll
-    for (int r = 0; r < NB; ++r) { Wr[r] = 0.0; Wi[r] = 0.0; }
-
-    // ---- initial window W_k(s0) = Σ_{j=s0}^{s0+N-1} x[j] w^{kj}: four independent accumulator /
-    // twiddle chains (samples j = 4m + p) so the dependent FMA and twiddle recurrences overlap
     const double2 wk4 = twiddle((4 * (int64_t)kb) % N, N);
     const double2 wkp[3] = {wk, twiddle((2 * (int64_t)kb) % N, N), twiddle((3 * (int64_t)kb) % N, N)};
-    const int64_t s0 = o0 + a.cp;
-    {
-        double Pr[4][NB], Pi[4][NB];
+
+    double Wr[NB], Wi[NB];
+    const int nblk = (a.chunk > 0 && N % a.chunk == 0) ? (int)(N / a.chunk) : 0;
+    if (nblk >= 1 && nblk <= ZF_NBLK) {
+        // ---- shared block sums: blocks c_first .. c_last + nblk - 1 of this stream, round-robin
+        const int64_t c_last = min(c_first + ZF_WAVES, a.nchunks) - 1;
+        const int nb_needed = (int)(c_last - c_first) + nblk;
+        double2* blk = reinterpret_cast<double2*>(lds);           // [block][NB][64]
+        for (int m = wave; m < nb_needed; m += ZF_WAVES) {
+            double br_[NB], bi_[NB];
+            zf_window<FMT, NB>(a, b, a.cp + (c_first + m) * a.chunk, a.chunk, lane, kb, wk, wk4, wkp, br_, bi_);
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-            for (int r = 0; r < NB; ++r) { Pr[p][r] = 0.0; Pi[p][r] = 0.0; }
-        for (int64_t j0 = s0; j0 < s0 + N; j0 += 64) {
-            const int cnt = (int)min((int64_t)64, s0 + N - j0);
-            double xr[NB], xi[NB];
-#pragma unroll
-            for (int r = 0; r < NB; ++r) {
-                double2 v = make_double2(0.0, 0.0);
-                if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
-                xr[r] = v.x; xi[r] = v.y;
-            }
-            double2 tw[4];
-            tw[0] = twiddle(((int64_t)kb * j0) % N, N);                 // exact anchor per block
-#pragma unroll
-            for (int p = 1; p < 4; ++p)
-                tw[p] = make_double2(tw[0].x * wkp[p - 1].x - tw[0].y * wkp[p - 1].y,
-                                     tw[0].x * wkp[p - 1].y + tw[0].y * wkp[p - 1].x);
-            if (cnt == 64) {
-#pragma unroll 4
-                for (int u = 0; u < 64; u += 4) {
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-#pragma unroll
-                        for (int r = 0; r < NB; ++r) {
-                            const double ur = ofs::readlane(xr[r], u + p), ui = ofs::readlane(xi[r], u + p);
-                            Pr[p][r] = fma(ur, tw[p].x, fma(-ui, tw[p].y, Pr[p][r]));
-                            Pi[p][r] = fma(ur, tw[p].y, fma(ui, tw[p].x, Pi[p][r]));
-                        }
-                        const double nr = tw[p].x * wk4.x - tw[p].y * wk4.y;
-                        const double ni = tw[p].x * wk4.y + tw[p].y * wk4.x;
-                        tw[p].x = nr; tw[p].y = ni;
-                    }
-                }
-            } else {
-                double2 t = tw[0];
-                for (int u = 0; u < cnt; ++u) {
-#pragma unroll
-                    for (int r = 0; r < NB; ++r) {
-                        const double ur = ofs::readlane(xr[r], u), ui = ofs::readlane(xi[r], u);
-                        Pr[0][r] = fma(ur, t.x, fma(-ui, t.y, Pr[0][r]));
-                        Pi[0][r] = fma(ur, t.y, fma(ui, t.x, Pi[0][r]));
-                    }
-                    const double nr = t.x * wk.x - t.y * wk.y;
-                    const double ni = t.x * wk.y + t.y * wk.x;
-                    t.x = nr; t.y = ni;
-                }
-            }
+            for (int r = 0; r < NB; ++r) blk[(m * NB + r) * 64 + lane] = make_double2(br_[r], bi_[r]);
         }
+        __syncthreads();
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
-            Wr[r] = (Pr[0][r] + Pr[1][r]) + (Pr[2][r] + Pr[3][r]);
-            Wi[r] = (Pi[0][r] + Pi[1][r]) + (Pi[2][r] + Pi[3][r]);
+            double sr = 0.0, si = 0.0;
+            if (c <= c_last)
+                for (int q = 0; q < nblk; ++q) {
+                    const double2 v = blk[((wave + q) * NB + r) * 64 + lane];
+                    sr += v.x; si += v.y;
+                }
+            Wr[r] = sr; Wi[r] = si;
         }
+        __syncthreads();                                          // blk is the transpose buffer below
+        if (c > c_last) return;
+    } else {
+        if (c >= a.nchunks) return;                               // no barriers on this path
+        zf_window<FMT, NB>(a, b, o0 + a.cp, N, lane, kb, wk, wk4, wkp, Wr, Wi);
     }
+    double (*red)[ZF_G][17] = reinterpret_cast<double (*)[ZF_G][17]>(lds + wave * 3 * ZF_G * 17);
 
-    // ---- slide over the chunk, 64 offsets per transpose group
+    // ---- slide over the chunk, ZF_G offsets per transpose group
+    double2 tw = make_double2(1.0, 0.0);
+    int64_t anchor = o0 - ZF_ANCHOR;
     for (int64_t og = o0; og < o1; og += ZF_G) {
         const int cnt = (int)min((int64_t)ZF_G, o1 - og);
         const int64_t sg = og + a.cp;
@@ -402,7 +447,7 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
             if (lane < cnt && sg + N + lane < a.T) vb = ld_c<FMT, double>(a.x, row + sg + N + lane);
             ar[r] = va.x; ai[r] = va.y; br_[r] = vb.x; bi[r] = vb.y;
         }
-        double2 tw = twiddle(((int64_t)kb * sg) % N, N);
+        if (og - anchor >= ZF_ANCHOR) { tw = twiddle(((int64_t)kb * sg) % N, N); anchor = og; }
         for (int u = 0; u < cnt; ++u) {
             double sr = 0.0, si = 0.0, e = 0.0;
 #pragma unroll
@@ -417,9 +462,9 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
             e *= emask;
             cr = quad_sum(cr); ci = quad_sum(ci); e = quad_sum(e);
             if ((lane & 3) == 0) {
-                red[wave][0][u][lane >> 2] = cr;
-                red[wave][1][u][lane >> 2] = ci;
-                red[wave][2][u][lane >> 2] = e;
+                red[0][u][lane >> 2] = cr;
+                red[1][u][lane >> 2] = ci;
+                red[2][u][lane >> 2] = e;
             }
 #pragma unroll
             for (int r = 0; r < NB; ++r) {                // W(s+1) = W(s) + (x[s+N]-x[s]) w^{ks}
@@ -437,9 +482,9 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
             double Cr = 0.0, Ci = 0.0, E = 0.0;
 #pragma unroll
             for (int g = 0; g < 16; ++g) {
-                Cr += red[wave][0][lane][g];
-                Ci += red[wave][1][lane][g];
-                E += red[wave][2][lane][g];
+                Cr += red[0][lane][g];
+                Ci += red[1][lane][g];
+                E += red[2][lane][g];
             }
             const double den = a.t_energy * E;
             static_cast<double*>(a.metric)[b * a.noff + og + lane] = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
@@ -972,8 +1017,7 @@ static bool zw_ok(int in_fmt, int precision, int N, int64_t noff) {
 
 template <int FMT>
 static int zf_launch(const ZfArgs& a, int nb, hipStream_t st) {
-    const int64_t items = a.B * a.nchunks;
-    const dim3 grid((unsigned)((items + ZF_WAVES - 1) / ZF_WAVES));
+    const dim3 grid((unsigned)(a.B * ((a.nchunks + ZF_WAVES - 1) / ZF_WAVES)));   // a stream's chunk groups
     switch (nb) {
         case 1: hipLaunchKernelGGL((zc_freq_kernel<FMT, 1>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
         case 2: hipLaunchKernelGGL((zc_freq_kernel<FMT, 2>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
@@ -1069,8 +1113,10 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
         return zw_launch(a, n_br, st);
     }
     if (n_br > 4) return OFS_EINVAL;
+    // chunks of offsets: halve from ~N while the grid has fewer than OFS_ZF_ITEMS chunks in all
+    static const int64_t zf_items = getenv("OFS_ZF_ITEMS") ? atoll(getenv("OFS_ZF_ITEMS")) : 4096;
     int64_t chunk = ((std::max<int64_t>(N, 256) + 63) / 64) * 64;
-    while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < 4096) chunk = ((chunk / 2 + 63) / 64) * 64;
+    while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < zf_items) chunk = ((chunk / 2 + 63) / 64) * 64;
     a.chunk = chunk;
     a.nchunks = (noff + chunk - 1) / chunk;
     switch (in_fmt) {
