@@ -19,6 +19,7 @@
 //     (block scan), the phase-slope fit and all means are block reductions.
 // Per-frame, O(N log N) work: compute-bound and tiny next to the metric kernels.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 #include "ofdmsync.h"
@@ -30,7 +31,7 @@ constexpr int BW = 256;
 constexpr int BNMAX = 4096;
 
 struct BeArgs {
-    int fmt; const void* x; int64_t T; int nb; int N, cp, n_used; double fs;
+    int fmt; const void* x; int64_t B, T; int nb; int N, cp, n_used; double fs;
     const int64_t* pilot_start; const int64_t* data_start; const double* cfo_in;
     const int32_t* bins; const double2* pilot; int64_t pilot_stride; const double2* data; int64_t data_stride;
     double* cfo_out; double2* h_out; double2* xa_out; double2* gain_out; double* evm_out; double* evm_db_out;
@@ -89,38 +90,61 @@ __device__ __forceinline__ double np_mod(double a, double b) {
     return m;
 }
 
-// N-point forward DFT of buf (natural order in / out) in LDS; tw[j] = exp(-2 pi i j / N)
+// N-point forward DFT of buf (bit-reversed in, natural order out) in LDS; tw[j] = exp(-2 pi i j / N).
+// Iterative radix-2 DIT, two stages fused per pass: a thread takes the four elements p, p+h,
+// p+2h, p+3h of a 4h-group and applies the len-2h butterflies then the len-4h ones in registers -
+// the same operations in the same order as two radix-2 passes (bit-identical), half the passes,
+// barriers and LDS round trips.  An odd stage count starts with one radix-2 pass.
 __device__ void fft_lds(double2* buf, const double2* tw, int N, int LB) {
-    for (int len = 2; len <= N; len <<= 1) {
-        const int half = len >> 1, step = N / len;
+    int len = 2;
+    if (LB & 1) {                                            // len-2 stage alone (w = 1)
         for (int j = threadIdx.x; j < N / 2; j += BW) {
-            const int g = j / half, k = j - g * half;
-            const int p = g * len + k, q = p + half;
-            const double2 t = cmul(tw[k * step], buf[q]);
-            const double2 u = buf[p];
-            buf[p] = make_double2(u.x + t.x, u.y + t.y);
-            buf[q] = make_double2(u.x - t.x, u.y - t.y);
+            const double2 u = buf[2 * j], v = buf[2 * j + 1];
+            const double2 t = cmul(tw[0], v);
+            buf[2 * j] = make_double2(u.x + t.x, u.y + t.y);
+            buf[2 * j + 1] = make_double2(u.x - t.x, u.y - t.y);
+        }
+        __syncthreads();
+        len = 4;
+    }
+    for (; len <= N; len <<= 2) {                            // stages len (h = len/2) and 2*len
+        const int h = len >> 1;
+        const int s1 = N / len, s2 = N / (2 * len);          // twiddle strides of the two stages
+        for (int j = threadIdx.x; j < N / 4; j += BW) {
+            const int g = j / h, k = j - g * h;
+            const int p = g * 4 * h + k;
+            const double2 a0 = buf[p], a1 = buf[p + h], a2 = buf[p + 2 * h], a3 = buf[p + 3 * h];
+            const double2 w1 = tw[k * s1];
+            const double2 t1 = cmul(w1, a1), t3 = cmul(w1, a3);
+            const double2 b0 = make_double2(a0.x + t1.x, a0.y + t1.y), b1 = make_double2(a0.x - t1.x, a0.y - t1.y);
+            const double2 b2 = make_double2(a2.x + t3.x, a2.y + t3.y), b3 = make_double2(a2.x - t3.x, a2.y - t3.y);
+            const double2 u = cmul(tw[k * s2], b2), v = cmul(tw[(k + h) * s2], b3);
+            buf[p] = make_double2(b0.x + u.x, b0.y + u.y);
+            buf[p + 2 * h] = make_double2(b0.x - u.x, b0.y - u.y);
+            buf[p + h] = make_double2(b1.x + v.x, b1.y + v.y);
+            buf[p + 3 * h] = make_double2(b1.x - v.x, b1.y - v.y);
         }
         __syncthreads();
     }
-    (void)LB;
 }
 
 __device__ __forceinline__ int bitrev(int v, int bits) { return (int)(__brev((unsigned)v) >> (32 - bits)); }
 
-// load rx_eff[s : s + N] = mean_br(rx[br] * exp(-i 2 pi cfo n / fs)) bit-reversed into buf
+// load rx_eff[s : s + N] = mean_br(rx[br] * exp(-i 2 pi cfo n / fs)) bit-reversed into buf.  The
+// tone of a thread's samples n = tid + BW·m comes from one sincos at its first sample and a
+// rotation by exp(i·phase(BW)) per step (angle addition: <= N/BW steps, ~1e-15 relative)
 template <int FMT>
 __device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, double2* buf, int LB) {
     const double w0 = 2.0 * M_PI * (-cfo);
+    double sn, cs, ss, cc;
+    sincos(w0 * (double)(s + (int64_t)threadIdx.x) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    sincos(w0 * (double)BW / a.fs, &ss, &cc);
+    double2 tone = make_double2(cs, sn);
+    const double2 step = make_double2(cc, ss);
     for (int n = threadIdx.x; n < a.N; n += BW) {
         const int64_t i = s + n;
         double2 acc = make_double2(0.0, 0.0);
         if (i >= 0 && i < a.T) {
-            // tone = exp(1j*2*pi*cfo*n/fs) as core.apply_cfo evaluates it (n = absolute index)
-            const double ph = w0 * (double)i / a.fs;
-            double sn, cs;
-            sincos(ph, &sn, &cs);
-            const double2 tone = make_double2(cs, sn);
             for (int br = 0; br < a.nb; ++br) {
                 const double2 v = cmul(ld<FMT>(a.x, (b * a.nb + br) * a.T + i), tone);
                 acc.x += v.x; acc.y += v.y;
@@ -128,6 +152,7 @@ __device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, d
             acc.x /= (double)a.nb; acc.y /= (double)a.nb;              // np.mean over branches
         }
         buf[bitrev(n, LB)] = acc;
+        tone = cmul(tone, step);
     }
     __syncthreads();
 }
@@ -141,13 +166,14 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
     double2* tw = bsm + a.N;                  // N / 2
     double2* hs = tw + a.N / 2;               // n_used: h, later xhat
     double* ph = reinterpret_cast<double*>(hs + a.n_used);   // n_used: phase / unwrap
-    const int64_t b = blockIdx.x;
     const int N = a.N, U = a.n_used, LB = 31 - __clz(N);
-    for (int j = threadIdx.x; j < N / 2; j += BW) {
+    for (int j = threadIdx.x; j < N / 2; j += BW) {             // once per workgroup
         double sn, cs;
         sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
         tw[j] = make_double2(cs, sn);
     }
+    for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {    // frames, grid-stride
+    __syncthreads();
     // ---- CFO (core.py:179-196) or given ----
     const int64_t ps = a.pilot_start[b];
     double cfo;
@@ -274,6 +300,7 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
         if (a.evm_out) a.evm_out[b] = evm;
         if (a.evm_db_out) a.evm_db_out[b] = 20.0 * log10(evm + 1e-12);
     }
+    }
 }
 
 }  // namespace
@@ -291,7 +318,7 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         pilot_stride < 0 || data_stride < 0 || B > 0x7fffffff)
         return OFS_EINVAL;
     if (B == 0) return OFS_OK;
-    BeArgs a{in_fmt, x, T, n_br, n_fft, cp_len, n_used, fs_hz, pilot_start, data_start, cfo_in, bins,
+    BeArgs a{in_fmt, x, B, T, n_br, n_fft, cp_len, n_used, fs_hz, pilot_start, data_start, cfo_in, bins,
              static_cast<const double2*>(pilot_used), pilot_stride, static_cast<const double2*>(data_used),
              data_stride, cfo_out, static_cast<double2*>(h_out), static_cast<double2*>(xa_out),
              static_cast<double2*>(gain_out), evm_out, evm_db_out, slope_out, sto_out};
@@ -301,7 +328,14 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return OFS_EHIP;
-        hipLaunchKernelGGL(kern, dim3((unsigned)B), dim3(BW), lds, st, a);
+        // resident workgroups only; each walks frames with a grid stride (one twiddle table each)
+        int dev = 0, cus = 256, per = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, BW, lds) != hipSuccess)
+            return OFS_EHIP;
+        const int64_t grid = std::min<int64_t>(B, (int64_t)cus * std::max(per, 1));
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BW), lds, st, a);
         return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
     };
     switch (in_fmt) {
