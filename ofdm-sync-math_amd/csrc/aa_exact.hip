@@ -320,7 +320,7 @@ struct RtlExactArgs {
 // induction from lane 0).  After round r lanes 0..r are exact, so it ends within 64 rounds
 // (the sequential cost); in practice the guessed trajectories coincide with the exact one
 // inside a chunk or two and a segment takes a few rounds.  The integer floor-shift RTL mode
-// (not contractive to the bit) runs sequentially.
+// (not contractive to the bit) runs in a walker lane per stream instead (rtl_walk).
 #ifndef OFS_RTL_SC
 #define OFS_RTL_SC 4
 #endif

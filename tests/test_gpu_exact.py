@@ -81,7 +81,7 @@ def _rtl_run(xt, Q, monkeypatch, exact, **kw):
 
 @pytest.mark.parametrize("B,nb,T,Q", [(33, 1, 1024, 64), (7, 2, 777, 64), (5, 3, 3000, 128),
                                       (4, 1, 4096, 512), (6, 2, 2500, 256)])
-@pytest.mark.parametrize("mode,shift,hyst", [("float", 3, 2), ("floor", 3, 2), ("float", 0, 0)])
+@pytest.mark.parametrize("mode,shift,hyst", [("float", 3, 2), ("floor", 3, 2), ("float", 0, 0), ("floor", 0, 1), ("floor", 6, 3)])
 def test_rtl_exact_kernel_bit_identical_to_general_engine(B, nb, T, Q, mode, shift, hyst, monkeypatch):
     rng = np.random.default_rng(B + Q + shift)
     iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q)))
