@@ -85,6 +85,10 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 // ds_read_b128.  Paired A/B on the same buffers: registers 1-3 % faster (profiles/
 // r01c_staging_ab.log; the SOL probe shows the same 8 % gap between LDS-DMA and register staging
 // of this read/write pattern).
+// scan-free gate flags in the P/R/M-storing instantiation too (tuning builds: -DOFS_FAST_FF=1)
+#ifndef OFS_FAST_FF
+#define OFS_FAST_FF 0
+#endif
 // DO: detect-only instantiation (P/R/M/valid not stored, events only: SURVEY §8d)
 template <int E, int MR, int NA, bool DO>
 __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
@@ -150,7 +154,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     double Cr[RW + 1], Ci[RW + 1], Ce[RW + 1];  // running row bases (wave-uniform)
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
-    AaRowGate<E, float, false, DO> gate;        // event state (wave-uniform)
+    AaRowGate<E, float, false, (bool)(DO || OFS_FAST_FF)> gate;   // event state (wave-uniform)
     if (a.detect)
         gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
                   a.ev_r + b * (int64_t)a.max_ev * 4);
