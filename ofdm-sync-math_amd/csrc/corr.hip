@@ -280,7 +280,10 @@ __global__ __launch_bounds__(CW) void zc_mf_kernel(ZcArgs a) {
 // B_k(m) = Σ_{j in block m} x[j] w^{kj}, and neighbouring chunks share all but one block: the
 // workgroup computes its ZF_WAVES + N/chunk - 1 blocks once (spread over its waves) and each
 // wave adds up its N/chunk of them (vs N samples per wave for a direct window).
-constexpr int ZF_WAVES = 4;
+#ifndef OFS_ZF_WAVES
+#define OFS_ZF_WAVES 4
+#endif
+constexpr int ZF_WAVES = OFS_ZF_WAVES;
 constexpr int ZF_NBLK = 8;
 // offsets per transpose group: the [3][ZF_G][17] fp64 LDS transpose buffer per wave sets the
 // occupancy (64 with 2-wave workgroups: 52 KiB = 6 waves per CU)
