@@ -69,10 +69,27 @@ struct ZGate {
     int open, nev;
 };
 
+// DMA: the walker stages the c / c[i-W] tiles with LDS-DMA (global_load_lds_dwordx4, no
+// registers), two chunks ahead of use instead of one (the register path's loads land one chunk
+// period after they are issued, so a chunk could not be shorter than a memory round trip);
+// taken when every tile row is a whole, 16-byte-aligned 1 KiB span (host checks).
+constexpr int ZDMA_PER_CHUNK = 2 * ZS * (ZC / 128);   // DMA instructions per chunk (c and c[i-W])
+
+// One LDS-DMA (64 lanes x 16 B -> LDS[lds .. lds + 1 KiB)), issued as inline asm: through the
+// builtin the compiler guards every later LDS read with a vmcnt(0) wait (it cannot tell which
+// LDS the DMA writes), which would drain the DMAs in flight and, in the helper waves, their own
+// global stores.  The kernel orders the DMAs itself (the walker's vmcnt waits + the barrier).
+__device__ __forceinline__ void lds_dma16(const void* g, const void* lds) {
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
+}
+
+template <bool DMA>
 __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
 #pragma clang fp contract(off)
-    __shared__ double tc[3][ZS][ZP];      // c
-    __shared__ double to[2][ZS][ZP];      // c[i - W] (0 before the window fills)
+    constexpr int NC = DMA ? 4 : 3, NO = DMA ? 3 : 2;
+    __shared__ double tc[NC][ZS][ZP];     // c
+    __shared__ double to[NO][ZS][ZP];     // c[i - W] (0 before the window fills)
     __shared__ double ta[2][ZS][ZP];      // running sum after sample i
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -105,9 +122,25 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
         for (int rr = 0; rr < ZR; ++rr)
 #pragma unroll
             for (int s = 0; s < ZS; ++s) {
-                tc[q % 3][s][64 * rr + lane] = pc[rr][s];
-                to[q & 1][s][64 * rr + lane] = po[rr][s];
+                tc[q % NC][s][64 * rr + lane] = pc[rr][s];
+                to[q % NO][s][64 * rr + lane] = po[rr][s];
             }
+    };
+    // DMA path: 1 KiB per instruction (64 lanes x 16 B); rows of absent streams re-read the last
+    // stream (unused); c[i-W] tiles of chunks before the window fills copy the c tile (the walker
+    // uses zeros there: W is a whole number of chunks on this path)
+    auto dma = [&](int q) {
+#pragma unroll
+        for (int s = 0; s < ZS; ++s) {
+            const int ss = s < ns ? s : ns - 1;
+            const double* src = cw + (int64_t)ss * n + (int64_t)q * ZC + 2 * lane;
+            const double* srco = (int64_t)q * ZC >= a.W ? src - a.W : src;
+#pragma unroll
+            for (int j = 0; j < ZC / 128; ++j) {
+                lds_dma16(src + 128 * j, &tc[q % NC][s][128 * j]);
+                lds_dma16(srco + 128 * j, &to[q % NO][s][128 * j]);
+            }
+        }
     };
 
     ZGate g[(ZS + ZH - 1) / ZH];
@@ -119,27 +152,53 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
     // would drain them, a full store round trip per chunk); the loads are staged one iteration
     // after they are issued, so their wait overlaps a whole chunk of work
     auto lds_barrier = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if constexpr (DMA) {
+            // no memory-model fence here: with LDS-DMA in the kernel the compiler implements a
+            // "local" release fence as vmcnt(0), which would drain the DMAs in flight (and the
+            // helpers' stores) every chunk.  This wave's LDS accesses complete at lgkmcnt(0); the
+            // DMA'd tiles a chunk reads were waited for by the walker before the barrier.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        }
     };
     if (wv == 0) {
-        load(0);
-        stage(0);
-        if (1 < nch) load(1);
+        if constexpr (DMA) {
+            dma(0);
+            if (1 < nch) dma(1);
+        } else {
+            load(0);
+            stage(0);
+            if (1 < nch) load(1);
+        }
     }
     lds_barrier();
     for (int q = 0; q <= nch; ++q) {
         if (wv == 0) {
-            if (q + 1 < nch) stage(q + 1);                    // loaded during the previous chunk
-            if (q + 2 < nch) load(q + 2);
+            if constexpr (DMA) {
+                if (q + 2 < nch) dma(q + 2);
+                // chunk q has landed once at most the (up to two) later chunks' DMAs are in flight
+                static_assert(ZDMA_PER_CHUNK == 16, "vmcnt immediates below assume 16 DMAs per chunk");
+                const int later = min(2, nch - 1 - q);
+                if (later >= 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                else if (later == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                if (q + 1 < nch) stage(q + 1);                // loaded during the previous chunk
+                if (q + 2 < nch) load(q + 2);
+            }
         }
         if (wv == 0) {
             // ---- walker: the exact left-to-right recursion of RunningSum.step ----
             if (!OFS_ZC_NOWALK && q < nch && lane < ZS) {
                 const int cnt = (int)min((int64_t)ZC, n - (int64_t)q * ZC);
-                const double* x = tc[q % 3][lane];
-                const double* o = to[q & 1][lane];
+                const double* x = tc[q % NC][lane];
+                const double* o = to[q % NO][lane];
+                const bool ozero = DMA && (int64_t)q * ZC < a.W;      // DMA path: before the window fills
                 double* r = ta[q & 1][lane];
                 if (cnt == ZC) {
                     // LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per
@@ -150,6 +209,7 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                     for (int j = 0; j < ZB / 2; ++j) {
                         xv[j] = reinterpret_cast<const double2*>(x)[j];
                         ov[j] = reinterpret_cast<const double2*>(o)[j];
+                        if (ozero) ov[j] = make_double2(0.0, 0.0);
                     }
 #pragma unroll
                     for (int bb = 0; bb < ZC / ZB; ++bb) {
@@ -159,6 +219,7 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                             for (int j = 0; j < ZB / 2; ++j) {
                                 xn[j] = reinterpret_cast<const double2*>(x + (bb + 1) * ZB)[j];
                                 on[j] = reinterpret_cast<const double2*>(o + (bb + 1) * ZB)[j];
+                                if (ozero) on[j] = make_double2(0.0, 0.0);
                             }
                         }
 #pragma unroll
@@ -178,7 +239,7 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                         }
                     }
                 } else {
-                    for (int u = 0; u < cnt; ++u) { acc = (acc + x[u]) - o[u]; r[u] = acc; }
+                    for (int u = 0; u < cnt; ++u) { acc = (acc + x[u]) - (ozero ? 0.0 : o[u]); r[u] = acc; }
                 }
             }
         } else if (!OFS_ZC_NOHELP && q >= 1) {
@@ -195,7 +256,7 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                 const int s = (wv - 1) + ZH * j;
                 if (s >= ns) break;
                 ZGate& G = g[j];
-                const double c = tc[qc % 3][s][64 * rr + lane];
+                const double c = tc[qc % NC][s][64 * rr + lane];
                 const double ls = ta[qc & 1][s][64 * rr + lane];
                 const double cs = c * a.scale, th = ls * a.tv;
                 const bool ab = vd && (cs >= th) && (c >= a.minmag);
@@ -289,6 +350,9 @@ int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double 
     ZcArgs a{corr_mag, B, n, W, tv, scale, minmag, reflen, Hp, local_sum, corr_scaled, thresh_scaled,
              above, valid, gate_mask, max_ev, n_ev, ev, ev_v};
     const int64_t grid = (B + ZS - 1) / ZS;
-    hipLaunchKernelGGL(zc_cfar_kernel, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
+    const bool dma = ZC % 128 == 0 && n % ZC == 0 && W % ZC == 0 && W >= 0 &&
+                     (reinterpret_cast<uintptr_t>(corr_mag) & 15) == 0 && !getenv("OFS_ZC_NODMA");
+    if (dma) hipLaunchKernelGGL(zc_cfar_kernel<true>, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
+    else hipLaunchKernelGGL(zc_cfar_kernel<false>, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }

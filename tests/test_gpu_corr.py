@@ -171,10 +171,13 @@ def test_zc_detect_preamble_vs_reference_golden():
     assert np.array_equal(r.gate_mask, d["gate_mask"])
 
 
-@pytest.mark.parametrize("hyst", [0, 1, 5, 64])
-def test_zc_cfar_and_gate_bit_identical_given_corr_mag(hyst):
-    rng = np.random.default_rng(hyst)
-    B, n, W = 4, 3000, 128
+@pytest.mark.parametrize("hyst,B,n,W", [(0, 4, 3000, 128), (1, 4, 3000, 128), (5, 4, 3000, 128), (64, 4, 3000, 128),
+                                         (64, 11, 4096, 256), (100, 9, 2048, 128), (64, 5, 1536, 512)])
+def test_zc_cfar_and_gate_bit_identical_given_corr_mag(hyst, B, n, W):
+    """CFAR + gate vs the oracle, bit for bit: the sequential kernel (hysteresis < 64), the fused
+    lane-per-stream kernel with register-staged tiles (n not a whole number of chunks) and with
+    LDS-DMA tiles (n and W whole chunks; 11 and 9 streams leave a workgroup's rows unused)."""
+    rng = np.random.default_rng(hyst + n)
     mag = np.abs(rng_c(rng, B, n)) * 0.2
     for b in range(B):
         for p in rng.integers(W, n - 50, size=6):
