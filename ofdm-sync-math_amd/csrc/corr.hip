@@ -752,9 +752,7 @@ __global__ __launch_bounds__(64 * Z64_WAVES, 1) void zc_win64_kernel(Zw64Args a,
     auto dma = [&](const float2* xs) {                          // 32 x 1 KiB, linear copy
 #pragma unroll
         for (int j = 0; j < 32; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(xs + 128 * j + 2 * lane),
-                                             (__attribute__((address_space(3))) void*)(slot + 128 * j),
-                                             16, 0, 0);
+            ofs::lds_dma16(xs + 128 * j + 2 * lane, slot + 128 * j);      // stays in flight (ofs_common.h)
     };
     int64_t item = (int64_t)blockIdx.x * Z64_WAVES + wave;
     int br = 0;
@@ -785,6 +783,10 @@ __global__ __launch_bounds__(64 * Z64_WAVES, 1) void zc_win64_kernel(Zw64Args a,
                 const float2 v = xs[64 * q + lane];
                 xv[q] = pf2{v.x, v.y};
             }
+            // consume the loads here, before the next unit's DMA is issued: the compiler's own
+            // vmcnt waits for them would otherwise count the (inline-asm) DMAs as well and drain them
+#pragma unroll
+            for (int q = 0; q < 64; ++q) asm volatile("" : "+v"(xv[q]));
         }
         staged = false;
         if (nitem < items) {                                    // prefetch the next unit

@@ -208,6 +208,18 @@ __device__ __forceinline__ RowScan row_scan(float v) {
 #endif
 }
 
+
+// One LDS-DMA: lane l's 16 bytes at g -> LDS[lds + 16 l] (64 lanes = 1 KiB), issued as inline asm.
+// Through __builtin_amdgcn_global_load_lds the compiler cannot tell which LDS the DMA writes, so
+// it guards every later LDS read with vmcnt(0) (and implements a "local" release fence as
+// vmcnt(0)), draining DMAs meant to stay in flight - and, in waves that also store to global
+// memory, those stores.  Callers order the DMAs themselves: s_waitcnt vmcnt(n) in the issuing wave
+// before the data is read (and a barrier before other waves read it).
+__device__ __forceinline__ void lds_dma16(const void* g, const void* lds) {
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
+}
+
 }  // namespace ofs
 
 // internal launchers implemented in aa_fast.hip (C++ linkage, not part of the ABI)

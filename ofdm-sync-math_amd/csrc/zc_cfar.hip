@@ -75,15 +75,6 @@ struct ZGate {
 // taken when every tile row is a whole, 16-byte-aligned 1 KiB span (host checks).
 constexpr int ZDMA_PER_CHUNK = 2 * ZS * (ZC / 128);   // DMA instructions per chunk (c and c[i-W])
 
-// One LDS-DMA (64 lanes x 16 B -> LDS[lds .. lds + 1 KiB)), issued as inline asm: through the
-// builtin the compiler guards every later LDS read with a vmcnt(0) wait (it cannot tell which
-// LDS the DMA writes), which would drain the DMAs in flight and, in the helper waves, their own
-// global stores.  The kernel orders the DMAs itself (the walker's vmcnt waits + the barrier).
-__device__ __forceinline__ void lds_dma16(const void* g, const void* lds) {
-    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds;
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
-}
-
 template <bool DMA>
 __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
 #pragma clang fp contract(off)
