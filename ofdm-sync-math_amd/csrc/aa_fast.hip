@@ -84,7 +84,9 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 // stream into a private 8 KiB LDS slice (global_load_lds_dwordx4) and reads rows back with
 // ds_read_b128.  Paired A/B on the same buffers: registers 1-3 % faster (profiles/
 // r01c_staging_ab.log; the SOL probe shows the same 8 % gap between LDS-DMA and register staging
-// of this read/write pattern).
+// of this read/write pattern).  Round 2, with the DMA as inline asm and per-row vmcnt waits (the
+// builtin made the compiler wait for the whole stream before the first row) and 107 instead of
+// 139 VGPRs (4 waves/SIMD): still 3 % slower (0.315 vs 0.305 ms, profiles/r02av_staging_ab.jsonl).
 // scan-free gate flags in the P/R/M-storing instantiation too (tuning builds: -DOFS_FAST_FF=1)
 #ifndef OFS_FAST_FF
 #define OFS_FAST_FF 0
@@ -106,21 +108,31 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     if (b >= a.B) return;
     const int T = (int)a.T;
 #if OFS_FAST_STAGE == 0
+    // row-major DMA order (row k of every antenna before row k+1): row k has landed once at most
+    // the later rows' DMAs and the output stores of rows < k (SPR per row, all younger) are
+    // outstanding - vmcnt counts in order.  The DMA goes through inline asm (ofs::lds_dma16): the
+    // builtin makes the compiler wait for every DMA before the first LDS read.  Event stores are
+    // not counted (a larger count could only under-wait; a smaller one waits longer).
+    constexpr int SPR = V4 + ((E % 4 != 0) ? 2 * V4 : 2 * (V4 / 2));   // P + R + M stores per row
 #pragma unroll
-    for (int t = 0; t < NA; ++t) {
-        const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * NA + t) * a.T;
+    for (int k = 0; k < RW; ++k)
 #pragma unroll
-        for (int k = 0; k < RW; ++k)
+        for (int t = 0; t < NA; ++t) {
+            const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * NA + t) * a.T;
 #pragma unroll
             for (int j = 0; j < V4; ++j) {
                 int n = RL * k + E * lane + 2 * j;
                 n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
-                __builtin_amdgcn_global_load_lds((const void*)(xs + n),
-                                                 (__attribute__((address_space(3))) void*)&lds[w][(t * RW + k) * V4 + j][0],
-                                                 16, 0, OFS_DMA_AUX);
+                ofs::lds_dma16(xs + n, &lds[w][(t * RW + k) * V4 + j][0]);
             }
-    }
+        }
     auto ldrow = [&](int t, int k, int j) { return lds[w][(t * RW + k) * V4 + j][lane]; };
+    // SPR counts only when all of P, R, M are stored (uncounted stores only make the wait longer)
+    const bool all_out = !DO && a.P && a.R && a.M;
+    auto row_wait = [&](int k) {
+        if (all_out) ofs::vmcnt_wait((RW - 1 - k) * NA * V4 + k * SPR);
+        else ofs::vmcnt_wait((RW - 1 - k) * NA * V4);
+    };
 #else
     // register staging: every row of the lane's samples is loaded up front (RW * V4 float4), each
     // row's first use waits only for its own loads (vmcnt counts in order)
@@ -138,6 +150,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
             }
     }
     auto ldrow = [&](int t, int k, int j) { return xreg[t][k][j]; };
+    auto row_wait = [&](int) {};
 #endif
     auto xrow = [&](int t, int k, pf2 (&c)[E]) {
 #pragma unroll
@@ -175,6 +188,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
             float aE[E];
 #pragma unroll
             for (int e = 0; e < E; ++e) { av[e] = pf2{0.f, 0.f}; aE[e] = 0.f; }
+            row_wait(k);
 #pragma unroll
             for (int t = 0; t < NA; ++t) {
                 pf2 c[E];

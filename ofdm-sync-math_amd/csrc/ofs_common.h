@@ -220,6 +220,25 @@ __device__ __forceinline__ void lds_dma16(const void* g, const void* lds) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
 }
 
+
+// s_waitcnt vmcnt(n) for an n that folds to a constant at compile time (unrolled loops); n > 63
+// waits for the hardware maximum (63), i.e. at least as long
+#define OFS_VMW(i) case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+__device__ __forceinline__ void vmcnt_wait(int n) {
+    switch (n < 63 ? n : 63) {
+        OFS_VMW(0) OFS_VMW(1) OFS_VMW(2) OFS_VMW(3) OFS_VMW(4) OFS_VMW(5) OFS_VMW(6) OFS_VMW(7)
+        OFS_VMW(8) OFS_VMW(9) OFS_VMW(10) OFS_VMW(11) OFS_VMW(12) OFS_VMW(13) OFS_VMW(14) OFS_VMW(15)
+        OFS_VMW(16) OFS_VMW(17) OFS_VMW(18) OFS_VMW(19) OFS_VMW(20) OFS_VMW(21) OFS_VMW(22) OFS_VMW(23)
+        OFS_VMW(24) OFS_VMW(25) OFS_VMW(26) OFS_VMW(27) OFS_VMW(28) OFS_VMW(29) OFS_VMW(30) OFS_VMW(31)
+        OFS_VMW(32) OFS_VMW(33) OFS_VMW(34) OFS_VMW(35) OFS_VMW(36) OFS_VMW(37) OFS_VMW(38) OFS_VMW(39)
+        OFS_VMW(40) OFS_VMW(41) OFS_VMW(42) OFS_VMW(43) OFS_VMW(44) OFS_VMW(45) OFS_VMW(46) OFS_VMW(47)
+        OFS_VMW(48) OFS_VMW(49) OFS_VMW(50) OFS_VMW(51) OFS_VMW(52) OFS_VMW(53) OFS_VMW(54) OFS_VMW(55)
+        OFS_VMW(56) OFS_VMW(57) OFS_VMW(58) OFS_VMW(59) OFS_VMW(60) OFS_VMW(61) OFS_VMW(62)
+        default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+    }
+}
+#undef OFS_VMW
+
 }  // namespace ofs
 
 // internal launchers implemented in aa_fast.hip (C++ linkage, not part of the ABI)
