@@ -371,6 +371,14 @@ __device__ __forceinline__ void rtl_walk(const double* __restrict__ wcp, double*
     for (; li < n; ++li) wes[seg_at(li)] = step(wcp[seg_at(li)], wes[seg_at(li)]);
 }
 
+// workgroup barrier ordering LDS only: a __syncthreads() fence would also wait for every global
+// store in flight (vmcnt(0)), a store round trip per segment
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <int E, int MW, int CPNA, int NBM>
 __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #pragma clang fp contract(off)
@@ -391,7 +399,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const bool walk = seq && smode == 2;        // the RTL floor IIR runs in a walker lane (barriers)
     if (b >= a.B) {                 // no stream: still meet the workgroup's two barriers per segment
         if (walk)
-            for (int64_t g = 0; g < (T + SEG - 1) / SEG; ++g) { __syncthreads(); __syncthreads(); }
+            for (int64_t g = 0; g < (T + SEG - 1) / SEG; ++g) { lds_barrier(); lds_barrier(); }
         return;
     }
     double* hae_ = rsm + wave_dbl * w;
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             // written: wave 0, lane t walking stream t through the segment's corr_positive /
             // energy_scaled in LDS (rtl_walk).  The smoothed value goes back over energy_scaled
             // with the threshold decision in its sign bit (the state is never negative).
-            __syncthreads();
+            lds_barrier();
             if (w == 0 && lane < wpb && (int64_t)blockIdx.x * wpb + lane < a.B) {
                 const double* wcp = rsm + wave_dbl * lane + 2 * NR * E * 64;
                 double* wes = const_cast<double*>(wcp) + SEG_PAD;
@@ -553,7 +561,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 const int v0 = (int)max((int64_t)0, min((int64_t)n, (int64_t)vstart - s0));
                 rtl_walk<2>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
             }
-            __syncthreads();
+            lds_barrier();
 #pragma unroll
             for (int e = 0; e < SC; ++e) {
                 const int64_t p = c0 + e;

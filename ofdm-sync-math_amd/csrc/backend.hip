@@ -65,14 +65,24 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
     return make_double2((a.x * r + a.y) / d, (a.y * r - a.x) / d);
 }
 
+// workgroup barrier ordering LDS only: every barrier here orders LDS traffic (the global inputs
+// are read-only and outputs are never read back), and a __syncthreads() fence would also wait
+// for the frame's output stores in flight (vmcnt(0)) at each of the ~45 barriers of a frame
+// (measured neutral here, r02aw: the frame's stores are few)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // block-wide sum of doubles (all threads get the result)
 __device__ double block_sum(double v, double* red) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    __syncthreads();
+    lds_barrier();
     if (lane == 0) red[w] = v;
-    __syncthreads();
+    lds_barrier();
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < BW / 64; ++k) s += red[k];
@@ -104,7 +114,7 @@ __device__ void fft_lds(double2* buf, const double2* tw, int N, int LB) {
             buf[2 * j] = make_double2(u.x + t.x, u.y + t.y);
             buf[2 * j + 1] = make_double2(u.x - t.x, u.y - t.y);
         }
-        __syncthreads();
+        lds_barrier();
         len = 4;
     }
     for (; len <= N; len <<= 2) {                            // stages len (h = len/2) and 2*len
@@ -124,7 +134,7 @@ __device__ void fft_lds(double2* buf, const double2* tw, int N, int LB) {
             buf[p + h] = make_double2(b1.x + v.x, b1.y + v.y);
             buf[p + 3 * h] = make_double2(b1.x - v.x, b1.y - v.y);
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -154,7 +164,7 @@ __device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, d
         buf[bitrev(n, LB)] = acc;
         tone = cmul(tone, step);
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 template <int FMT>
@@ -173,7 +183,7 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
         tw[j] = make_double2(cs, sn);
     }
     for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {    // frames, grid-stride
-    __syncthreads();
+    lds_barrier();
     // ---- CFO (core.py:179-196) or given ----
     const int64_t ps = a.pilot_start[b];
     double cfo;
@@ -210,7 +220,7 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
         ph[u] = atan2(h.y, h.x);
         if (a.h_out) a.h_out[b * U + u] = h;
     }
-    __syncthreads();
+    lds_barrier();
     // ---- phase slope (core.py:443-469): unwrap = p + cumsum(correction), then the LS fit ----
     {
         // each thread owns a contiguous run of bins; correction[u] applies to bins >= u
@@ -232,13 +242,13 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
             if (lane >= d) incl += t;
         }
         if (lane == 63) scan_tot[w] = incl;
-        __syncthreads();
+        lds_barrier();
         double base = incl - local;
         for (int k = 0; k < w; ++k) base += scan_tot[k];
-        __syncthreads();
+        lds_barrier();
         // rewrite ph[u] = unwrapped phase (reads of ph[u-1] done above, before the barrier)
         double run = base, prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
-        __syncthreads();
+        lds_barrier();
         for (int u = u0; u < u1; ++u) {
             const double raw = ph[u];
             if (u >= 1) {
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
             prev_raw = raw;
             ph[u] = raw + run;
         }
-        __syncthreads();
+        lds_barrier();
     }
     double sk = 0.0, sp = 0.0;
     for (int u = threadIdx.x; u < U; u += BW) { sk += (double)a.bins[u]; sp += ph[u]; }
