@@ -24,6 +24,10 @@
 namespace {
 
 constexpr int FW = 256;
+#ifndef OFS_MC_FX
+#define OFS_MC_FX 1024
+#endif
+constexpr int FX = OFS_MC_FX;     // extract workgroup (energy prefix + normalised outputs)
 
 struct McPlan {
     rocfft_plan fwd = nullptr, inv = nullptr;
@@ -100,10 +104,10 @@ __device__ double block_excl_scan(double v, double* red) {
 __device__ __forceinline__ int pidx(int m, int per) { return m + m / per; }
 
 template <int FMT>
-__global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
+__global__ __launch_bounds__(FX) void mc_extract_kernel(McArgs a) {
     extern __shared__ double pf[];
-    const int per = a.M / FW;                       // M is a power of two >= FW
-    const int plen = a.M + FW + 1;                  // padded prefix length per branch (M / per = FW pads)
+    const int per = a.M / FX;                       // M is a power of two >= FX
+    const int plen = a.M + FX + 1;                  // padded prefix length per branch (M / per = FX pads)
     double* red = pf + (size_t)a.nb * plen;
     const int64_t b = blockIdx.y, q = blockIdx.x;
     const int64_t n0 = q * a.S;
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
     for (int br = 0; br < a.nb; ++br) {
         const int64_t row = b * a.nb + br;
         double* P = pf + (size_t)br * plen;
-        for (int m = threadIdx.x; m < a.M; m += FW) {            // |x|^2, coalesced
+        for (int m = threadIdx.x; m < a.M; m += FX) {            // |x|^2, coalesced
             const int64_t g = g0 + m;
             double e = 0.0;
             if (g >= 0 && g < a.T) { const double2 v = ldx<FMT>(a.x, row * a.T + g); e = v.x * v.x + v.y * v.y; }
@@ -129,10 +133,10 @@ __global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
             P[i] = run;
             run += e;
         }
-        if (threadIdx.x == FW - 1) P[pidx(a.M, per)] = run;
+        if (threadIdx.x == FX - 1) P[pidx(a.M, per)] = run;
         __syncthreads();
     }
-    for (int s = threadIdx.x; s < ns; s += FW) {
+    for (int s = threadIdx.x; s < ns; s += FX) {
         double sr = 0.0, si = 0.0, se = 0.0;
         for (int br = 0; br < a.nb; ++br) {
             const int64_t row = b * a.nb + br;
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(FW) void mc_extract_kernel(McArgs a) {
     }
 }
 
-size_t extract_lds(int nb, int M) { return ((size_t)nb * (M + FW + 1) + FW / 64) * sizeof(double); }
+size_t extract_lds(int nb, int M) { return ((size_t)nb * (M + FX + 1) + FX / 64) * sizeof(double); }
 
 int pick_m(int N, int64_t T, int nb) {
     // overlap-save FFT size: power of two >= 2N minimising the transformed elements nblk·M
@@ -172,7 +176,7 @@ int pick_m(int N, int64_t T, int nb) {
     int best = 0;
     int64_t cost = INT64_MAX;
     for (int64_t M = 1; M <= (int64_t)1 << 16; M <<= 1) {
-        if (M < 2 * (int64_t)N || M < FW || extract_lds(nb, (int)M) > 160 * 1024) continue;
+        if (M < 2 * (int64_t)N || M < FW || M < FX || extract_lds(nb, (int)M) > 160 * 1024) continue;
         const int64_t S = M - N + 1, nblk = (nout + S - 1) / S;
         if (nblk * M < cost) { cost = nblk * M; best = (int)M; }
     }
@@ -192,7 +196,7 @@ extern "C" {
 int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_br, int64_t T, int32_t M,
                               void** plan_out, size_t* work_bytes, size_t* scratch_bytes) {
     if (!ref || !plan_out || N < 1 || B < 1 || n_br < 1 || T < 1 || M < 0 || (M && (M & (M - 1))) ||
-        (M && (M < 2 * N || M < FW)))
+        (M && (M < 2 * N || M < FW || M < FX)))
         return OFS_EINVAL;
     *plan_out = nullptr;
     if (!M) M = pick_m(N, T, n_br);
@@ -308,19 +312,19 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
             if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C64>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FW), lds, st, a);
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FX), lds, st, a);
             break;
         case OFS_C128:
             if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C128>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FW), lds, st, a);
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FX), lds, st, a);
             break;
         default:
             if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_CI16>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
                 return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FW), lds, st, a);
+            hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FX), lds, st, a);
             break;
     }
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
