@@ -27,7 +27,10 @@
 
 namespace {
 
-constexpr int BW = 256;
+#ifndef OFS_BE_WG
+#define OFS_BE_WG 256
+#endif
+constexpr int BW = OFS_BE_WG;     // threads per frame workgroup
 constexpr int BNMAX = 4096;
 
 struct BeArgs {
