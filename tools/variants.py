@@ -31,6 +31,7 @@ def main():
             so = os.path.join(OUT, f"libofdmsync_{name}.so")
             G.link_lib([*objs, f.result()], so, "variant-" + name)
             print(so)
+    G.build_hip()       # keep the in-tree library in step with the sources (tests load it unbuilt)
 
 
 if __name__ == "__main__":
