@@ -301,7 +301,8 @@ int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
  * and normalised per `mode` (OFS_ZC_RAW, _V2, _COMBINED, _SUM; as ofs_zc_correlate, the window
  * energy from an fp64 prefix over each block; ref_energy as ofs_zc_correlate).  The plan is made
  * for one reference (host c128, N taps) and one batch shape; `scratch` must hold *scratch_bytes (the [rows * blocks][M] c128
- * spectra), `work` *work_bytes (rocFFT work area, may be 0).
+ * spectra), `work` *work_bytes (rocFFT work area, may be 0).  A plan carries its rocFFT execution
+ * state: use it from one host thread / stream at a time (one plan per concurrent caller).
  */
 int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_br, int64_t T, int32_t M,
                               void** plan_out, size_t* work_bytes, size_t* scratch_bytes);

@@ -37,6 +37,7 @@ struct McPlan {
     double ref_norm = 0.0;
     size_t work_bytes = 0;
     size_t scratch_bytes = 0;
+    rocfft_execution_info info = nullptr;   // reused by every call (stream / work buffer set per call)
 };
 
 std::once_flag g_setup;
@@ -254,6 +255,25 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
         delete p;
         return OFS_EFFT;
     }
+    // per-plan, once: the execution info and the extract kernels' LDS limit (per call they cost
+    // host time comparable to the whole GPU pipeline at this size)
+    const size_t lds = extract_lds(p->nb, p->M);
+    bool ok2 = rocfft_execution_info_create(&p->info) == rocfft_status_success;
+    if (ok2 && lds > 64 * 1024)
+        ok2 = hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds) == hipSuccess &&
+              hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds) == hipSuccess &&
+              hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_CI16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds) == hipSuccess;
+    if (!ok2) {
+        if (p->info) rocfft_execution_info_destroy(p->info);
+        rocfft_plan_destroy(p->fwd);
+        rocfft_plan_destroy(p->inv);
+        (void)hipFree(p->H);
+        delete p;
+        return OFS_EHIP;
+    }
     if (work_bytes) *work_bytes = p->work_bytes;
     if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
     *plan_out = p;
@@ -263,6 +283,7 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
 int32_t ofs_zc_mf_plan_destroy(void* plan) {
     McPlan* p = static_cast<McPlan*>(plan);
     if (!p) return OFS_OK;
+    if (p->info) rocfft_execution_info_destroy(p->info);
     if (p->fwd) rocfft_plan_destroy(p->fwd);
     if (p->inv) rocfft_plan_destroy(p->inv);
     if (p->H) (void)hipFree(p->H);
@@ -290,8 +311,7 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
         default: hipLaunchKernelGGL(mc_pack_kernel<OFS_CI16>, gp, dim3(FW), 0, st, a); break;
     }
     if (hipGetLastError() != hipSuccess) return OFS_EHIP;
-    rocfft_execution_info info = nullptr;
-    if (rocfft_execution_info_create(&info) != rocfft_status_success) return OFS_EFFT;
+    rocfft_execution_info info = p->info;
     rocfft_status s = rocfft_execution_info_set_stream(info, st);
     if (s == rocfft_status_success && p->work_bytes) s = rocfft_execution_info_set_work_buffer(info, work, p->work_bytes);
     void* io[1] = {scratch};
@@ -300,32 +320,16 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
         const int64_t n = rows * p->nblk * p->M;
         hipLaunchKernelGGL(mc_mul_kernel, dim3((unsigned)std::min<int64_t>((n + FW - 1) / FW, 1 << 20)), dim3(FW), 0, st,
                            static_cast<double2*>(scratch), p->H, n, p->M, 1.0 / (double)p->M);
-        if (hipGetLastError() != hipSuccess) { rocfft_execution_info_destroy(info); return OFS_EHIP; }
+        if (hipGetLastError() != hipSuccess) return OFS_EHIP;
         s = rocfft_execute(p->inv, io, nullptr, info);
     }
-    rocfft_execution_info_destroy(info);
     if (s != rocfft_status_success) return OFS_EFFT;
-    const size_t lds = extract_lds(n_br, p->M);
+    const size_t lds = extract_lds(n_br, p->M);      // its LDS limit was raised at plan creation
     const dim3 ge((unsigned)p->nblk, (unsigned)B);
     switch (in_fmt) {
-        case OFS_C64:
-            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C64>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FX), lds, st, a);
-            break;
-        case OFS_C128:
-            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C128>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FX), lds, st, a);
-            break;
-        default:
-            if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_CI16>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-                return OFS_EHIP;
-            hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FX), lds, st, a);
-            break;
+        case OFS_C64: hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FX), lds, st, a); break;
+        case OFS_C128: hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FX), lds, st, a); break;
+        default: hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FX), lds, st, a); break;
     }
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
