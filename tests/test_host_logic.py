@@ -90,3 +90,19 @@ def test_hex_vector_is_the_preamble():
     pre = synth.aa_preamble(1024)
     assert iq.shape == (1024, 2)
     assert np.array_equal(iq[:, 0], np.round(pre.real * 1024)) and np.array_equal(iq[:, 1], np.round(pre.imag * 1024))
+
+
+from ofdm_sync_amd import zc_freq  # noqa: E402
+
+
+def test_rocfft_default_chunk_sizing():
+    """Chunked rocFFT plans (zc_freq.default_chunk): a multiple of the branch count, sized to
+    about CHUNK_BYTES of spectrum, 0 (one execution) when one chunk would cover the batch."""
+    N, esz = 4096, 8
+    per = zc_freq.CHUNK_BYTES // (N * esz)
+    assert zc_freq.default_chunk(1 << 20, 1, N, esz) == per
+    c = zc_freq.default_chunk(1 << 20, 3, N, esz)
+    assert c % 3 == 0 and 0 < c <= per
+    assert zc_freq.default_chunk(per, 1, N, esz) == 0
+    assert zc_freq.default_chunk(10, 2, N, esz) == 0
+    assert zc_freq.default_chunk(1 << 20, 2, 1 << 26, 16) == 2        # never below one stream's branches
