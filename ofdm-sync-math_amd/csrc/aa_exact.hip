@@ -396,7 +396,10 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const bool seq = a.smooth || a.corr_scaled || a.above || a.detect;
     const size_t wave_dbl = rtl_wave_lds(E, MW, nb_) / sizeof(double);
     const int smode = a.smooth_mode == 1 ? 2 : (a.shift == 0 ? 1 : 0);
-    const bool walk = seq && smode == 2;        // the RTL floor IIR runs in a walker lane (barriers)
+#ifndef OFS_RTL_WALK_ALL                    // tuning builds: every smoothing mode in the walker
+#define OFS_RTL_WALK_ALL 0
+#endif
+    const bool walk = seq && (smode == 2 || OFS_RTL_WALK_ALL);   // RTL floor IIR: walker lane (barriers)
     if (b >= a.B) {                 // no stream: still meet the workgroup's two barriers per segment
         if (walk)
             for (int64_t g = 0; g < (T + SEG - 1) / SEG; ++g) { lds_barrier(); lds_barrier(); }
@@ -559,7 +562,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 double* wes = const_cast<double*>(wcp) + SEG_PAD;
                 const int n = (int)(send - s0);
                 const int v0 = (int)max((int64_t)0, min((int64_t)n, (int64_t)vstart - s0));
-                rtl_walk<2>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
+                if (smode == 2) rtl_walk<2>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
+                else if (smode == 1) rtl_walk<1>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
+                else rtl_walk<0>(wcp, wes, n, v0, inv, scale, a.shift, sm, si);
             }
             lds_barrier();
 #pragma unroll
