@@ -57,8 +57,9 @@ def parse(argv=None):
     ap.add_argument("--T", type=int, default=1024)
     ap.add_argument("--L", type=int, default=512)
     ap.add_argument("--max-events", type=int, default=4)
-    ap.add_argument("--placement", choices=("contiguous", "plain"), default="contiguous",
-                    help="sync_aa.allocate placement of the detector's buffers")
+    ap.add_argument("--placement", choices=("auto", "contiguous", "plain"), default="auto",
+                    help="AABatchDetector placement of the detector's buffers (the product default "
+                         "'auto'; the JSON line records the placement actually used)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=3.0, help="seconds per CPU leg")
@@ -307,7 +308,8 @@ def main(argv=None):
         "config": {"workload": "cfg3 Schmidl-Cox float32 metric+CFO, N=1024 (L=512), cir1, "
                                f"{B} streams x {T} c64 per GPU",
                    "global_batch": B_glob, "seq_len": T, "L": L,
-                   "parallelism": f"stream-shard x{world} (no collectives)", "placement": a.placement},
+                   "parallelism": f"stream-shard x{world} (no collectives)",
+                   "placement": a.placement if a.selftest_cpu else f"{a.placement} -> {det.placement}"},
     }
     if a.selftest_cpu:
         out.update(selftest=True, rank_ms=ms, shard=[lo, lo + B])

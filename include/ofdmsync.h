@@ -439,6 +439,63 @@ int32_t ofs_sc_gate(int32_t precision, const void* M_sc, int64_t B, int64_t n, d
 int32_t ofs_segment_peak(const double* Ms, const uint8_t* mask, int64_t B, int64_t n, int64_t bound_lo,
                          int64_t bound_hi, int64_t* peak, int32_t* status, void* stream);
 
+
+/* ------------------------------------------------------------------------------------------
+ * The receiver back-end helpers one by one (the reference drivers call them individually,
+ * sc.py:274-311), batched over rows, device pointers, c128 = interleaved (re, im) doubles.
+ * Row operands ("ref", "den") take a row stride in elements (0 = one row shared by all).
+ * ------------------------------------------------------------------------------------------ */
+
+/* core.ofdm_fft_used (core.py:171-176): out[b][u] = fftshift(fft(x[b], n=n_fft))[(n_fft/2 +
+ * bins[u]) % n_fft] = DFT_n_fft of x[b][0 : min(T, n_fft)] zero-padded, at bin bins[u] mod n_fft
+ * (numpy's fft(x, n) truncates or zero-pads).  x [B][T] c64/c128/int16 I/Q; bins [n_used] int32
+ * (device); out c128 [B][n_used]; n_fft a power of two <= 4096.  fp64 radix-2 FFT in LDS. */
+int32_t ofs_fft_used(int32_t in_fmt, const void* x, int64_t B, int64_t T, int32_t n_fft, int32_t n_used,
+                     const int32_t* bins, void* out, void* stream);
+
+/* core.ls_channel_estimate (core.py:339-341) and core.equalize (:344-345): out = num / (den + eps)
+ * with numpy's complex128 division (Smith's algorithm with the reciprocal scale, no contraction:
+ * bit-identical to numpy).  num, out [B][n] c128; den [.][n] c128 with row stride den_stride. */
+int32_t ofs_cdiv_eps(const void* num, int64_t B, int64_t n, const void* den, int64_t den_stride, double eps,
+                     void* out, void* stream);
+
+/* core.remove_common_phase (core.py:348-354): cpe = angle(mean(x)) when ref is NULL, else
+ * angle(vdot(ref, x) / (vdot(ref, ref) + 1e-12)); out = x * exp(-i cpe).  x [B][n] c128;
+ * ref [.][n] c128 (ref_stride) or NULL; cpe [B] f64; out [B][n] c128 (nullable). */
+int32_t ofs_common_phase(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, void* out,
+                         double* cpe, void* stream);
+
+/* core.align_complex_gain (core.py:357-362): g = vdot(x, ref) / (vdot(x, x) + eps); out = x * g.
+ * gain [B] c128; out [B][n] c128 (nullable). */
+int32_t ofs_align_gain(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, double eps,
+                       void* out, void* gain, void* stream);
+
+/* core.evm_rms_db (core.py:365-370): evm = sqrt(mean|x - ref|^2 / mean|ref|^2),
+ * evm_db = 20 log10(evm + 1e-12).  evm, evm_db [B] f64 (each nullable). */
+int32_t ofs_evm(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, double* evm,
+                double* evm_db, void* stream);
+
+/* core.estimate_timing_offset_from_phase_slope (core.py:443-469): phi = unwrap(angle(h)) (numpy's
+ * unwrap rule), slope = Σ (k - k̄)(phi - phī) / (Σ (k - k̄)² + 1e-12) over the abscissa bins[u]
+ * (centred subcarrier indices), sto = -slope * n_fft / (2 pi).  h [B][n_used] c128; slope, sto
+ * [B] f64 (each nullable). */
+int32_t ofs_phase_slope(const void* h, int64_t B, int32_t n_used, const int32_t* bins, int32_t n_fft,
+                        double* slope, double* sto, void* stream);
+
+/* core.apply_cfo (core.py:123-138): out[b][br][n] = x[b][br][n] * exp(i phi_n), phi_n =
+ * ((2 pi cfo_b) n) * (1 / fs) - the reference's operation order (its complex scalar arithmetic
+ * reduces to these two products); one tone per stream, shared by its branches.  x [B][n_br][T]
+ * c64/c128/int16 I/Q; cfo_hz [B] f64 (device); out c128 [B][n_br][T]. */
+int32_t ofs_apply_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T, const double* cfo_hz,
+                      double fs_hz, void* out, void* stream);
+
+/* sync_aa.quantize_adc (sync_aa.py:263-291): per component v -> round(clip(v / fs, -1, 1 - 1/L) * L)
+ * / L * fs, L = 2^(bits-1), round half to even (np.round).  precision OFS_FP32: complex64 in and
+ * out, every operation in fp32 (numpy 2 keeps float32 when full_scale is a Python float);
+ * OFS_FP64: c64 or c128 in, c128 out (a float64 full_scale promotes).  Bit-identical to numpy. */
+int32_t ofs_quantize_adc(int32_t in_fmt, const void* x, int64_t n, double full_scale, int32_t bits,
+                         int32_t precision, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

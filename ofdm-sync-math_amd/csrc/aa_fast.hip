@@ -590,15 +590,23 @@ int launch_e(int E, int mr, const AaFastArgs& a, hipStream_t st) {
 }
 
 int pick_e(int L) {
-    // samples per lane per row; override for tuning with OFS_FAST_E=2|4|8
-    static int forced = -1;
-    if (forced < 0) {
-        const char* s = getenv("OFS_FAST_E");
-        forced = s ? atoi(s) : 0;
-    }
+    // samples per lane per row; override for tuning with OFS_FAST_E=2|4|8 (read per call)
+    const char* s = getenv("OFS_FAST_E");
+    const int forced = s ? atoi(s) : 0;
     if (forced == 2 || forced == 4 || forced == 8) return (L % (64 * forced) == 0) ? forced : 0;
     for (int e : {2, 4, 8})                                  // E=2 measured 3 % faster than 4 (r01c)
         if (L % (64 * e) == 0) return e;
+    return 0;
+}
+
+// detect-only (events without P/R/M stores: VALU/issue-bound, not HBM-bound, SQ counters r03a):
+// samples per lane per row.  Wider rows amortise the three fp64 DPP row scans (lane totals of
+// Re P, Im P, R: ~25 VALU each per row) over more samples; override with OFS_FAST_E_DO=2|4|8.
+int pick_e_do(int L) {
+    const char* s = getenv("OFS_FAST_E_DO");
+    const int forced = s ? atoi(s) : 0;
+    for (int e : {forced, 8, 4, 2})
+        if ((e == 2 || e == 4 || e == 8) && L % (64 * e) == 0) return e;
     return 0;
 }
 
@@ -631,7 +639,12 @@ int ofs_aa_fast_try(int fmt, int precision, int n_ant, const AaFastArgs& a, hipS
         if (E == 2) return n_ant == 1 ? launch_stream_mr<2, 1>(mr, a, st) : launch_stream_mr<2, 2>(mr, a, st);
         return n_ant == 1 ? launch_stream_mr<4, 1>(mr, a, st) : launch_stream_mr<4, 2>(mr, a, st);
     }
-    // detect-only keeps the full call's E (events identical to the full call's, same arithmetic);
-    // E = 4 would be ~8 % faster there (paired A/B r02w: 0.134 -> 0.119 ms)
-    return n_ant == 1 ? launch_e<1>(plan / 10, plan % 10, a, st) : launch_e<2>(plan / 10, plan % 10, a, st);
+    int E = plan / 10, mr = plan % 10;
+    if (a.detect && !a.P && !a.R && !a.M && !a.valid) {
+        // detect-only: its own row width (fewer fp64 row scans per sample); the events are those of
+        // the same window sums in another fp32 summation order (parity: oracle/parity.py criterion)
+        const int ed = pick_e_do(a.L);
+        if (ed) { E = ed; mr = a.L / (64 * ed); }
+    }
+    return n_ant == 1 ? launch_e<1>(E, mr, a, st) : launch_e<2>(E, mr, a, st);
 }

@@ -57,15 +57,18 @@ __device__ __forceinline__ double2 ld(const void* p, int64_t i) {
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-// a / b, Smith's algorithm (scaled; the form numpy's complex division uses)
+// a / b exactly as numpy divides complex128 (Smith's algorithm with the reciprocal scale
+// scl = 1 / (b.x + b.y * rat), no contraction): bit-identical to numpy on the same operands
 __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
-    if (fabs(b.x) >= fabs(b.y)) {
-        if (b.x == 0.0 && b.y == 0.0) return make_double2(a.x / fabs(b.x), a.y / fabs(b.y));
-        const double r = b.y / b.x, d = b.x + b.y * r;
-        return make_double2((a.x + a.y * r) / d, (a.y - a.x * r) / d);
+#pragma clang fp contract(off)
+    const double br = fabs(b.x), bi = fabs(b.y);
+    if (br >= bi) {
+        if (br == 0.0 && bi == 0.0) return make_double2(a.x / br, a.y / bi);
+        const double rat = b.y / b.x, scl = 1.0 / (b.x + b.y * rat);
+        return make_double2((a.x + a.y * rat) * scl, (a.y - a.x * rat) * scl);
     }
-    const double r = b.x / b.y, d = b.y + b.x * r;
-    return make_double2((a.x * r + a.y) / d, (a.y * r - a.x) / d);
+    const double rat = b.x / b.y, scl = 1.0 / (b.y + b.x * rat);
+    return make_double2((a.x * rat + a.y) * scl, (a.y * rat - a.x) * scl);
 }
 
 // workgroup barrier ordering LDS only: every barrier here orders LDS traffic (the global inputs
@@ -139,6 +142,64 @@ __device__ void fft_lds(double2* buf, const double2* tw, int N, int LB) {
         }
         lds_barrier();
     }
+}
+
+// estimate_timing_offset_from_phase_slope (core.py:443-469) on ph[0..U) = angle(h) in LDS (all
+// threads): np.unwrap restated as per-bin corrections (numpy's float mod and boundary rule) and
+// an exclusive block scan - ph becomes the unwrapped phase - then the LS slope over the abscissa
+// bins[u].  Ends with the workgroup converged (block_sum).
+__device__ double unwrap_slope(double* ph, const int32_t* bins, int U, double* red, double* scan_tot) {
+    {
+        // each thread owns a contiguous run of bins; correction[u] applies to bins >= u
+        const int per = (U + BW - 1) / BW;
+        const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
+        double local = 0.0;
+        for (int u = max(u0, 1); u < u1; ++u) {
+            const double dd = ph[u] - ph[u - 1];
+            double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+            if (dm == -M_PI && dd > 0.0) dm = M_PI;
+            local += fabs(dd) < M_PI ? 0.0 : dm - dd;
+        }
+        // exclusive block scan of the per-thread totals
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        double incl = local;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double t = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        if (lane == 63) scan_tot[w] = incl;
+        lds_barrier();
+        double base = incl - local;
+        for (int k = 0; k < w; ++k) base += scan_tot[k];
+        lds_barrier();
+        // rewrite ph[u] = unwrapped phase (reads of ph[u-1] done above, before the barrier)
+        double run = base, prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
+        lds_barrier();
+        for (int u = u0; u < u1; ++u) {
+            const double raw = ph[u];
+            if (u >= 1) {
+                const double dd = raw - prev_raw;
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                run += fabs(dd) < M_PI ? 0.0 : dm - dd;
+            }
+            prev_raw = raw;
+            ph[u] = raw + run;
+        }
+        lds_barrier();
+    }
+    double sk = 0.0, sp = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) { sk += (double)bins[u]; sp += ph[u]; }
+    const double kmean = block_sum(sk, red) / (double)U;
+    const double pmean = block_sum(sp, red) / (double)U;
+    double skk = 0.0, skp = 0.0;
+    for (int u = threadIdx.x; u < U; u += BW) {
+        const double kz = (double)bins[u] - kmean, pz = ph[u] - pmean;
+        skk += kz * kz; skp += kz * pz;
+    }
+    const double den = block_sum(skk, red) + 1e-12;
+    return block_sum(skp, red) / den;
 }
 
 __device__ __forceinline__ int bitrev(int v, int bits) { return (int)(__brev((unsigned)v) >> (32 - bits)); }
@@ -224,58 +285,8 @@ __global__ __launch_bounds__(BW) void rx_backend_kernel(BeArgs a) {
         if (a.h_out) a.h_out[b * U + u] = h;
     }
     lds_barrier();
-    // ---- phase slope (core.py:443-469): unwrap = p + cumsum(correction), then the LS fit ----
-    {
-        // each thread owns a contiguous run of bins; correction[u] applies to bins >= u
-        const int per = (U + BW - 1) / BW;
-        const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
-        double local = 0.0;
-        for (int u = max(u0, 1); u < u1; ++u) {
-            const double dd = ph[u] - ph[u - 1];
-            double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
-            if (dm == -M_PI && dd > 0.0) dm = M_PI;
-            local += fabs(dd) < M_PI ? 0.0 : dm - dd;
-        }
-        // exclusive block scan of the per-thread totals
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        double incl = local;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const double t = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += t;
-        }
-        if (lane == 63) scan_tot[w] = incl;
-        lds_barrier();
-        double base = incl - local;
-        for (int k = 0; k < w; ++k) base += scan_tot[k];
-        lds_barrier();
-        // rewrite ph[u] = unwrapped phase (reads of ph[u-1] done above, before the barrier)
-        double run = base, prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
-        lds_barrier();
-        for (int u = u0; u < u1; ++u) {
-            const double raw = ph[u];
-            if (u >= 1) {
-                const double dd = raw - prev_raw;
-                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
-                if (dm == -M_PI && dd > 0.0) dm = M_PI;
-                run += fabs(dd) < M_PI ? 0.0 : dm - dd;
-            }
-            prev_raw = raw;
-            ph[u] = raw + run;
-        }
-        lds_barrier();
-    }
-    double sk = 0.0, sp = 0.0;
-    for (int u = threadIdx.x; u < U; u += BW) { sk += (double)a.bins[u]; sp += ph[u]; }
-    const double kmean = block_sum(sk, red) / (double)U;
-    const double pmean = block_sum(sp, red) / (double)U;
-    double skk = 0.0, skp = 0.0;
-    for (int u = threadIdx.x; u < U; u += BW) {
-        const double kz = (double)a.bins[u] - kmean, pz = ph[u] - pmean;
-        skk += kz * kz; skp += kz * pz;
-    }
-    const double den = block_sum(skk, red) + 1e-12;
-    const double slope = block_sum(skp, red) / den;
+    // ---- phase slope (core.py:443-469) ----
+    const double slope = unwrap_slope(ph, a.bins, U, red, scan_tot);
     if (threadIdx.x == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
         if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
@@ -357,3 +368,291 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         default: return launch(rx_backend_kernel<OFS_CI16>);
     }
 }
+
+// ------------------------------------------------------------------------------------------
+// The back-end helpers one by one (include/ofdmsync.h): one 256-thread workgroup per row for
+// the FFT and the row reductions, grid-stride elementwise kernels for the rest.  fp64 except
+// quantize_adc's fp32 mode (numpy 2 keeps float32 there).
+// ------------------------------------------------------------------------------------------
+namespace {
+
+// core.ofdm_fft_used (core.py:171-176): fft(x, n=N) (truncate / zero-pad), fftshift, gather
+template <int FMT>
+__global__ __launch_bounds__(BW) void fft_used_kernel(const void* x, int64_t B, int64_t T, int N, int U,
+                                                      const int32_t* bins, double2* out) {
+    extern __shared__ __attribute__((aligned(16))) double2 fsm[];
+    double2* buf = fsm;
+    double2* tw = fsm + N;
+    const int LB = 31 - __clz(N);
+    for (int j = threadIdx.x; j < N / 2; j += BW) {
+        double sn, cs;
+        sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
+        tw[j] = make_double2(cs, sn);
+    }
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        lds_barrier();
+        for (int n = threadIdx.x; n < N; n += BW)
+            buf[bitrev(n, LB)] = n < T ? ld<FMT>(x, b * T + n) : make_double2(0.0, 0.0);
+        lds_barrier();
+        fft_lds(buf, tw, N, LB);
+        for (int u = threadIdx.x; u < U; u += BW) {
+            int k = bins[u] % N;
+            if (k < 0) k += N;
+            out[b * U + u] = buf[k];
+        }
+    }
+}
+
+__global__ void cdiv_eps_kernel(const double2* num, int64_t B, int64_t n, const double2* den, int64_t ds, double eps,
+                                double2* out) {
+    const int64_t total = B * n;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = i / n, j = i - b * n;
+        const double2 d = den[b * ds + j];
+        out[i] = cdiv(num[i], make_double2(d.x + eps, d.y));       // num / (den + eps)
+    }
+}
+
+// row reductions: remove_common_phase (OP 0), align_complex_gain (OP 1), evm_rms_db (OP 2)
+template <int OP>
+__global__ __launch_bounds__(BW) void row_kernel(const double2* x, int64_t B, int64_t n, const double2* ref,
+                                                 int64_t rs, double eps, double2* out, double* r0, double2* g_out,
+                                                 double* r1) {
+    __shared__ double red[BW / 64];
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        const double2* xr = x + b * n;
+        const double2* rr = ref ? ref + b * rs : nullptr;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (int64_t j = threadIdx.x; j < n; j += BW) {
+            const double2 v = xr[j];
+            if constexpr (OP == 0) {
+                if (rr) {                                    // vdot(ref, x), vdot(ref, ref)
+                    const double2 r = rr[j];
+                    s0 += r.x * v.x + r.y * v.y; s1 += r.x * v.y - r.y * v.x; s2 += r.x * r.x + r.y * r.y;
+                } else {
+                    s0 += v.x; s1 += v.y;                    // mean(x)
+                }
+            } else if constexpr (OP == 1) {                  // vdot(x, ref), vdot(x, x)
+                const double2 r = rr[j];
+                s0 += v.x * r.x + v.y * r.y; s1 += v.x * r.y - v.y * r.x; s2 += v.x * v.x + v.y * v.y;
+            } else {                                         // |x - ref|^2, |ref|^2
+                const double2 r = rr[j];
+                const double er = v.x - r.x, ei = v.y - r.y;
+                s0 += er * er + ei * ei; s2 += r.x * r.x + r.y * r.y;
+            }
+        }
+        s0 = block_sum(s0, red);
+        s1 = block_sum(s1, red);
+        s2 = block_sum(s2, red);
+        double2 rot;
+        if constexpr (OP == 0) {
+            double cpe;
+            if (rr) {
+                const double2 q = cdiv(make_double2(s0, s1), make_double2(s2 + 1e-12, 0.0));
+                cpe = atan2(q.y, q.x);
+            } else {
+                cpe = atan2(s1 / (double)n, s0 / (double)n);
+            }
+            if (threadIdx.x == 0 && r0) r0[b] = cpe;
+            double sn, cs;
+            sincos(cpe, &sn, &cs);
+            rot = make_double2(cs, -sn);                     // exp(-i cpe)
+        } else if constexpr (OP == 1) {
+            rot = cdiv(make_double2(s0, s1), make_double2(s2 + eps, 0.0));
+            if (threadIdx.x == 0 && g_out) g_out[b] = rot;
+        } else {
+            if (threadIdx.x == 0) {
+                const double evm = sqrt((s0 / (double)n) / (s2 / (double)n));
+                if (r0) r0[b] = evm;
+                if (r1) r1[b] = 20.0 * log10(evm + 1e-12);
+            }
+        }
+        if constexpr (OP != 2) {
+            if (out)
+                for (int64_t j = threadIdx.x; j < n; j += BW) out[b * n + j] = cmul(xr[j], rot);
+        }
+        lds_barrier();                                       // red reused by the next row
+    }
+}
+
+__global__ __launch_bounds__(BW) void phase_slope_kernel(const double2* h, int64_t B, int U, const int32_t* bins,
+                                                         int N, double* slope_out, double* sto_out) {
+    extern __shared__ double psm[];
+    __shared__ double red[BW / 64];
+    __shared__ double scan_tot[BW / 64];
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        lds_barrier();
+        for (int u = threadIdx.x; u < U; u += BW) {
+            const double2 v = h[b * U + u];
+            psm[u] = atan2(v.y, v.x);
+        }
+        lds_barrier();
+        const double slope = unwrap_slope(psm, bins, U, red, scan_tot);
+        if (threadIdx.x == 0) {
+            if (slope_out) slope_out[b] = slope;
+            if (sto_out) sto_out[b] = -slope * (double)N / (2.0 * M_PI);
+        }
+    }
+}
+
+// core.apply_cfo: phi = ((2 pi cfo) n) * (1 / fs), out = x * (cos phi + i sin phi)
+template <int FMT>
+__global__ void apply_cfo_kernel(const void* x, int64_t B, int nb, int64_t T, const double* cfo, double fs,
+                                 double2* out) {
+#pragma clang fp contract(off)
+    const double rfs = 1.0 / fs;
+    const int64_t total = B * nb * T;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / T, n = i - row * T, b = row / nb;
+        const double w = (2.0 * M_PI) * cfo[b];
+        const double ph = (w * (double)n) * rfs;
+        double sn, cs;
+        sincos(ph, &sn, &cs);
+        const double2 v = ld<FMT>(x, i);
+        out[i] = make_double2(v.x * cs - v.y * sn, v.x * sn + v.y * cs);
+    }
+}
+
+// sync_aa.quantize_adc, one component: round(clip(v / fs, -1, 1 - 1/L) * L) / L * fs
+template <class R>
+__device__ __forceinline__ R adc_q(R v, R fs, R L) {
+#pragma clang fp contract(off)
+    R s = v / fs;
+    const R hi = (R)1 - (R)1 / L;
+    s = s < (R)-1 ? (R)-1 : s;                       // np.clip(x, -1, hi) = minimum(maximum(x, -1), hi)
+    s = s > hi ? hi : s;
+    return rint(s * L) / L * fs;
+}
+
+template <class IN, class R, class OUT>
+__global__ void quantize_kernel(const IN* x, int64_t n, double full_scale, int bits, OUT* out) {
+    const R fs = (R)full_scale, L = (R)(1ll << (bits - 1));
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const IN v = x[i];
+        OUT o;
+        o.x = adc_q<R>((R)v.x, fs, L);
+        o.y = adc_q<R>((R)v.y, fs, L);
+        out[i] = o;
+    }
+}
+
+inline unsigned ew_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536)); }
+inline unsigned row_grid(int64_t B) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>(B, 8192)); }
+
+}  // namespace
+
+extern "C" {
+
+int32_t ofs_fft_used(int32_t in_fmt, const void* x, int64_t B, int64_t T, int32_t n_fft, int32_t n_used,
+                     const int32_t* bins, void* out, void* stream) {
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || OFS_MISSING(x, B * T) || B < 0 ||
+        T < 0 || n_fft < 2 || n_fft > BNMAX || (n_fft & (n_fft - 1)) || n_used < 1 || !bins || OFS_MISSING(out, B))
+        return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    const size_t lds = (size_t)n_fft * 16 + (size_t)(n_fft / 2) * 16;
+    hipStream_t st = (hipStream_t)stream;
+    auto launch = [&](auto kern) -> int32_t {
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return OFS_EHIP;
+        hipLaunchKernelGGL(kern, dim3(row_grid(B)), dim3(BW), lds, st, x, B, T, (int)n_fft, (int)n_used, bins,
+                           static_cast<double2*>(out));
+        return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+    };
+    switch (in_fmt) {
+        case OFS_C64: return launch(fft_used_kernel<OFS_C64>);
+        case OFS_C128: return launch(fft_used_kernel<OFS_C128>);
+        default: return launch(fft_used_kernel<OFS_CI16>);
+    }
+}
+
+int32_t ofs_cdiv_eps(const void* num, int64_t B, int64_t n, const void* den, int64_t den_stride, double eps,
+                     void* out, void* stream) {
+    if (B < 0 || n < 0 || den_stride < 0 || OFS_MISSING(num, B * n) || OFS_MISSING(den, B * n) ||
+        OFS_MISSING(out, B * n))
+        return OFS_EINVAL;
+    if (B == 0 || n == 0) return OFS_OK;
+    hipLaunchKernelGGL(cdiv_eps_kernel, dim3(ew_grid(B * n)), dim3(256), 0, (hipStream_t)stream,
+                       static_cast<const double2*>(num), B, n, static_cast<const double2*>(den), den_stride, eps,
+                       static_cast<double2*>(out));
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_common_phase(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, void* out,
+                         double* cpe, void* stream) {
+    if (B < 0 || n < 1 || ref_stride < 0 || OFS_MISSING(x, B) || OFS_MISSING(cpe, B)) return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    hipLaunchKernelGGL(row_kernel<0>, dim3(row_grid(B)), dim3(BW), 0, (hipStream_t)stream,
+                       static_cast<const double2*>(x), B, n, static_cast<const double2*>(ref), ref_stride, 0.0,
+                       static_cast<double2*>(out), cpe, (double2*)nullptr, (double*)nullptr);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_align_gain(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, double eps,
+                       void* out, void* gain, void* stream) {
+    if (B < 0 || n < 0 || ref_stride < 0 || OFS_MISSING(x, B) || OFS_MISSING(ref, B) || OFS_MISSING(gain, B))
+        return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    hipLaunchKernelGGL(row_kernel<1>, dim3(row_grid(B)), dim3(BW), 0, (hipStream_t)stream,
+                       static_cast<const double2*>(x), B, n, static_cast<const double2*>(ref), ref_stride, eps,
+                       static_cast<double2*>(out), (double*)nullptr, static_cast<double2*>(gain), (double*)nullptr);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_evm(const void* x, int64_t B, int64_t n, const void* ref, int64_t ref_stride, double* evm,
+                double* evm_db, void* stream) {
+    if (B < 0 || n < 0 || ref_stride < 0 || OFS_MISSING(x, B) || OFS_MISSING(ref, B)) return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    hipLaunchKernelGGL(row_kernel<2>, dim3(row_grid(B)), dim3(BW), 0, (hipStream_t)stream,
+                       static_cast<const double2*>(x), B, n, static_cast<const double2*>(ref), ref_stride, 0.0,
+                       (double2*)nullptr, evm, (double2*)nullptr, evm_db);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_phase_slope(const void* h, int64_t B, int32_t n_used, const int32_t* bins, int32_t n_fft,
+                        double* slope, double* sto, void* stream) {
+    if (B < 0 || n_used < 1 || n_used > 8192 || !bins || OFS_MISSING(h, B)) return OFS_EINVAL;
+    if (B == 0) return OFS_OK;
+    hipLaunchKernelGGL(phase_slope_kernel, dim3(row_grid(B)), dim3(BW), (size_t)n_used * 8, (hipStream_t)stream,
+                       static_cast<const double2*>(h), B, (int)n_used, bins, (int)n_fft, slope, sto);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_apply_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T, const double* cfo_hz,
+                      double fs_hz, void* out, void* stream) {
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128 || in_fmt == OFS_CI16) || B < 0 || n_br < 1 || T < 0 ||
+        OFS_MISSING(x, B * T) || OFS_MISSING(cfo_hz, B) || OFS_MISSING(out, B * T))
+        return OFS_EINVAL;
+    const int64_t total = B * n_br * T;
+    if (total == 0) return OFS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    double2* o = static_cast<double2*>(out);
+    switch (in_fmt) {
+        case OFS_C64: hipLaunchKernelGGL(apply_cfo_kernel<OFS_C64>, dim3(ew_grid(total)), dim3(256), 0, st, x, B, (int)n_br, T, cfo_hz, fs_hz, o); break;
+        case OFS_C128: hipLaunchKernelGGL(apply_cfo_kernel<OFS_C128>, dim3(ew_grid(total)), dim3(256), 0, st, x, B, (int)n_br, T, cfo_hz, fs_hz, o); break;
+        default: hipLaunchKernelGGL(apply_cfo_kernel<OFS_CI16>, dim3(ew_grid(total)), dim3(256), 0, st, x, B, (int)n_br, T, cfo_hz, fs_hz, o); break;
+    }
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+int32_t ofs_quantize_adc(int32_t in_fmt, const void* x, int64_t n, double full_scale, int32_t bits,
+                         int32_t precision, void* out, void* stream) {
+    if (!(in_fmt == OFS_C64 || in_fmt == OFS_C128) || n < 0 || bits < 1 || bits > 31 ||
+        !(precision == OFS_FP32 || precision == OFS_FP64) || (precision == OFS_FP32 && in_fmt != OFS_C64) ||
+        OFS_MISSING(x, n) || OFS_MISSING(out, n))
+        return OFS_EINVAL;
+    if (n == 0) return OFS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    if (precision == OFS_FP32)
+        hipLaunchKernelGGL((quantize_kernel<float2, float, float2>), dim3(ew_grid(n)), dim3(256), 0, st,
+                           static_cast<const float2*>(x), n, full_scale, (int)bits, static_cast<float2*>(out));
+    else if (in_fmt == OFS_C64)
+        hipLaunchKernelGGL((quantize_kernel<float2, double, double2>), dim3(ew_grid(n)), dim3(256), 0, st,
+                           static_cast<const float2*>(x), n, full_scale, (int)bits, static_cast<double2*>(out));
+    else
+        hipLaunchKernelGGL((quantize_kernel<double2, double, double2>), dim3(ew_grid(n)), dim3(256), 0, st,
+                           static_cast<const double2*>(x), n, full_scale, (int)bits, static_cast<double2*>(out));
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+
+}  // extern "C"

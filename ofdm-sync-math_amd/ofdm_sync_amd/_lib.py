@@ -34,12 +34,17 @@ def source_files() -> list[str]:
     return fs + ([_HDR] if os.path.exists(_HDR) else [])
 
 
+# hipcc flags of every translation unit (__graft_entry__.build_hip); part of the source hash, so a
+# flag change (arch, -O level, a -D knob) invalidates an existing library like a source edit
+BUILD_FLAGS = ("--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC")
+
+
 def source_hash() -> str:
-    """sha256 (16 hex digits) over the sources' names and bytes: baked into the library at
-    build time (OFS_SOURCE_HASH) and checked at load, so a library built from other sources
-    than the ones next to it is refused instead of silently run."""
+    """sha256 (16 hex digits) over the sources' names and bytes and the build flags: baked into
+    the library at build time (OFS_SOURCE_HASH) and checked at load, so a library built from
+    other sources or flags than the ones next to it is refused instead of silently run."""
     import hashlib
-    h = hashlib.sha256()
+    h = hashlib.sha256(" ".join(BUILD_FLAGS).encode() + b"\0")
     for f in source_files():
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
@@ -69,6 +74,14 @@ def _declare(lib):
                                  c_double, P, P, P]),
         "ofs_cp_search": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_int32, c_int32, c_int32,
                                     c_int32, c_double, P, P, P, P, P]),
+        "ofs_fft_used": (c_int32, [c_int32, P, c_int64, c_int64, c_int32, c_int32, P, P, P]),
+        "ofs_cdiv_eps": (c_int32, [P, c_int64, c_int64, P, c_int64, c_double, P, P]),
+        "ofs_common_phase": (c_int32, [P, c_int64, c_int64, P, c_int64, P, P, P]),
+        "ofs_align_gain": (c_int32, [P, c_int64, c_int64, P, c_int64, c_double, P, P, P]),
+        "ofs_evm": (c_int32, [P, c_int64, c_int64, P, c_int64, P, P, P]),
+        "ofs_phase_slope": (c_int32, [P, c_int64, c_int32, P, c_int32, P, P, P]),
+        "ofs_apply_cfo": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, P, c_double, P, P]),
+        "ofs_quantize_adc": (c_int32, [c_int32, P, c_int64, c_double, c_int32, c_int32, P, P]),
         "ofs_rx_backend": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, c_double, P, P,
                                      P, c_int32, P, P, c_int64, P, c_int64, P, P, P, P, P, P, P, P, P]),
         "ofs_synth_batch": (c_int32, [P, c_int64, c_int32, c_int64, c_int64, c_int32, c_double, c_double, c_double,
@@ -130,12 +143,16 @@ def lib():
                 f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
                 "from the repository root (hipcc --offload-arch=gfx950)")
         l = ctypes.CDLL(LIB_PATH)
-        _declare(l)
         if not os.environ.get("OFS_LIB") and source_files():
-            built, want = l.ofs_source_hash().decode(), source_hash()
+            fn = getattr(l, "ofs_source_hash", None)        # absent in libraries older than the check
+            if fn is not None:
+                fn.restype = ctypes.c_char_p
+                fn.argtypes = []
+            built, want = ("<none>" if fn is None else fn().decode()), source_hash()
             if built != want:
                 raise ImportError(f"{LIB_PATH} was built from other sources (hash {built}, sources {want}); "
                                   "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+        _declare(l)
         _lib = l
     return _lib
 

@@ -212,3 +212,192 @@ def receiver_backend(rx, pilot_cp_start: int, data_cp_start: int, pilot_used, da
         v = v[0].cpu()
         res[key] = v.numpy() if v.dim() else (complex(v.item()) if v.is_complex() else float(v.item()))
     return res
+
+
+# ---------------------------------------------------------------------------------------------
+# The back-end helpers one by one (core.py:123-138, 171-176, 339-370, 443-469), as the reference
+# drivers call them (sc.py:274-311).  Each has the reference's name, signature and return
+# convention (numpy in -> numpy out; torch in -> device tensors) and runs on the GPU; the
+# *_batched forms take [B, n] device rows.  The fused chain above stays the fast path.
+# ---------------------------------------------------------------------------------------------
+def _rows(a, dev, dtype=torch.complex128):
+    """(device tensor [B, n] of `dtype`, was_numpy, original ndim) for 1-D or 2-D input."""
+    from_numpy = not isinstance(a, torch.Tensor)
+    t = torch.as_tensor(np.asarray(a)) if from_numpy else a
+    nd = t.dim()
+    if nd not in (1, 2):
+        raise ValueError("expected a 1-D vector or [B, n] rows")
+    t = t.to(device=dev, dtype=dtype)
+    return (t[None] if nd == 1 else t).contiguous(), from_numpy, nd
+
+
+def _ref_rows(ref, B, n, dev):
+    """A reference operand broadcast like numpy against [B, n] rows: [n] shared (stride 0) or [B, n]."""
+    r = torch.as_tensor(np.asarray(ref)) if not isinstance(ref, torch.Tensor) else ref
+    r = r.to(device=dev, dtype=torch.complex128).contiguous()
+    if r.dim() == 1 and r.shape[0] == n:
+        return r, 0
+    if r.dim() == 2 and tuple(r.shape) == (B, n):
+        return r, n
+    raise ValueError(f"operands could not be broadcast together with shapes {(B, n)} {tuple(r.shape)}")
+
+
+def _out(t, from_numpy, nd):
+    t = t if nd == 2 else t[0]
+    return _lib.to_host(t) if from_numpy else t
+
+
+def apply_cfo_batched(x, cfo_hz, fs_hz: float) -> torch.Tensor:
+    """core.apply_cfo per stream of x[B, n_branch, T] with cfo_hz [B] (or a scalar) -> complex128."""
+    batch = _lib.as_batch(x, batched=True)
+    dev = batch.data.device
+    c = torch.as_tensor(np.asarray(cfo_hz, np.float64) if not isinstance(cfo_hz, torch.Tensor) else cfo_hz)
+    c = c.to(device=dev, dtype=torch.float64).reshape(-1)
+    if c.numel() == 1 and batch.B != 1:
+        c = c.expand(batch.B)
+    c = c.contiguous()
+    if c.numel() != batch.B:
+        raise ValueError("one cfo per stream expected")
+    out = torch.empty((batch.B, batch.nb, batch.T), dtype=torch.complex128, device=dev)
+    _lib.check(_lib.lib().ofs_apply_cfo(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, c.data_ptr(),
+                                        float(fs_hz), out.data_ptr(), _lib.stream_ptr()), "ofs_apply_cfo")
+    return out
+
+
+def apply_cfo(samples, cfo_hz: float, fs_hz: float):
+    """Apply a carrier frequency offset to 1D or 2D samples (core.py:123-138): axis 0 of a 2-D
+    input is branches, all rotated by the same tone exp(i 2 pi cfo n / fs)."""
+    from_numpy = not isinstance(samples, torch.Tensor)
+    a = np.asarray(samples) if from_numpy else samples
+    if a.ndim not in (1, 2):
+        raise ValueError("samples must be 1D or 2D")
+    if from_numpy and not np.iscomplexobj(a):
+        a = a.astype(np.complex128)
+    elif not from_numpy and not a.is_complex():
+        a = a.to(torch.complex128)
+    x = a[None] if a.ndim == 1 else a
+    out = apply_cfo_batched(x[None], [float(cfo_hz)], fs_hz)[0]
+    out = out[0] if a.ndim == 1 else out
+    return _lib.to_host(out) if from_numpy else out
+
+
+def ofdm_fft_used_batched(x, n_fft: int | None = None, bins=None) -> torch.Tensor:
+    """ofdm_fft_used of every row of x[B, T] -> complex128 [B, n_used] on the device."""
+    batch = _lib.as_batch(x, batched=True)
+    if batch.nb != 1:
+        raise ValueError("ofdm_fft_used_batched takes rows [B, T]")
+    N = int(N_FFT if n_fft is None else n_fft)
+    k = centered_subcarrier_indices(NUM_ACTIVE_SUBCARRIERS) if bins is None else np.asarray(bins)
+    kb = torch.as_tensor(k.astype(np.int32)).to(batch.data.device)
+    out = torch.empty((batch.B, k.size), dtype=torch.complex128, device=batch.data.device)
+    _lib.check(_lib.lib().ofs_fft_used(batch.fmt, batch.data.data_ptr(), batch.B, batch.T, N, int(k.size),
+                                       kb.data_ptr(), out.data_ptr(), _lib.stream_ptr()), "ofs_fft_used")
+    return out
+
+
+def ofdm_fft_used(symbol_time_no_cp):
+    """FFT an OFDM symbol (no CP) and return only used, centered subcarriers (core.py:171-176);
+    N_FFT and NUM_ACTIVE_SUBCARRIERS are read from this module at call time."""
+    from_numpy = not isinstance(symbol_time_no_cp, torch.Tensor)
+    a = np.asarray(symbol_time_no_cp) if from_numpy else symbol_time_no_cp
+    if a.ndim != 1:
+        raise ValueError("ofdm_fft_used takes one symbol (1-D samples)")
+    out = ofdm_fft_used_batched(a[None])[0]
+    return _lib.to_host(out) if from_numpy else out
+
+
+def _cdiv(y, d, eps):
+    dev = _lib.require_gpu()
+    t, from_numpy, nd = _rows(y, dev)
+    B, n = t.shape
+    r, rs = _ref_rows(d, B, n, dev)
+    out = torch.empty_like(t)
+    _lib.check(_lib.lib().ofs_cdiv_eps(t.data_ptr(), B, n, r.data_ptr(), rs, float(eps), out.data_ptr(),
+                                       _lib.stream_ptr()), "ofs_cdiv_eps")
+    return _out(out, from_numpy, nd)
+
+
+def ls_channel_estimate(y_used, x_used, eps: float = 1e-9):
+    """Least-squares per-subcarrier channel estimate H = Y / (X + eps) (core.py:339-341),
+    numpy's complex division bit for bit.  [B, n] rows with a shared [n] X broadcast."""
+    return _cdiv(y_used, x_used, eps)
+
+
+def equalize(y_used, h_est, eps: float = 1e-9):
+    """Y / (H + eps) (core.py:344-345), numpy's complex division bit for bit."""
+    return _cdiv(y_used, h_est, eps)
+
+
+def remove_common_phase(x, ref=None):
+    """De-rotate by the common phase error (core.py:348-354): the angle of mean(x), or of
+    vdot(ref, x) / (vdot(ref, ref) + 1e-12) when ref is given.  Returns (x * exp(-i cpe), cpe);
+    for [B, n] rows cpe is a [B] array / tensor."""
+    dev = _lib.require_gpu()
+    t, from_numpy, nd = _rows(x, dev)
+    B, n = t.shape
+    if n == 0:                                          # np.mean of nothing: nan
+        cpe = float("nan")
+        return (x.copy() if from_numpy else x.clone()), cpe
+    r, rs = _ref_rows(ref, B, n, dev) if ref is not None else (None, 0)
+    out = torch.empty_like(t)
+    cpe = torch.empty((B,), dtype=torch.float64, device=dev)
+    _lib.check(_lib.lib().ofs_common_phase(t.data_ptr(), B, n, _lib.ptr(r), rs, out.data_ptr(), cpe.data_ptr(),
+                                           _lib.stream_ptr()), "ofs_common_phase")
+    c = float(cpe[0].item()) if nd == 1 else (_lib.to_host(cpe) if from_numpy else cpe)
+    return _out(out, from_numpy, nd), c
+
+
+def align_complex_gain(x, ref, eps: float = 1e-12):
+    """Scale x by the complex gain g = vdot(x, ref) / (vdot(x, x) + eps) that best fits ref in
+    the LS sense (core.py:357-362).  Returns (x * g, g)."""
+    dev = _lib.require_gpu()
+    t, from_numpy, nd = _rows(x, dev)
+    B, n = t.shape
+    r, rs = _ref_rows(ref, B, n, dev)
+    out = torch.empty_like(t)
+    g = torch.empty((B,), dtype=torch.complex128, device=dev)
+    _lib.check(_lib.lib().ofs_align_gain(t.data_ptr(), B, n, r.data_ptr(), rs, float(eps), out.data_ptr(),
+                                         g.data_ptr(), _lib.stream_ptr()), "ofs_align_gain")
+    gg = complex(g[0].item()) if nd == 1 else (_lib.to_host(g) if from_numpy else g)
+    return _out(out, from_numpy, nd), gg
+
+
+def evm_rms_db(x, ref):
+    """(evm_rms, evm_db), EVM normalised to the reference RMS magnitude (core.py:365-370)."""
+    dev = _lib.require_gpu()
+    t, from_numpy, nd = _rows(x, dev)
+    B, n = t.shape
+    r, rs = _ref_rows(ref, B, n, dev)
+    evm = torch.empty((B,), dtype=torch.float64, device=dev)
+    db = torch.empty((B,), dtype=torch.float64, device=dev)
+    if n == 0:
+        evm.fill_(float("nan"))
+        db.fill_(float("nan"))
+    else:
+        _lib.check(_lib.lib().ofs_evm(t.data_ptr(), B, n, r.data_ptr(), rs, evm.data_ptr(), db.data_ptr(),
+                                      _lib.stream_ptr()), "ofs_evm")
+    if nd == 1:
+        return float(evm[0].item()), float(db[0].item())
+    return (_lib.to_host(evm), _lib.to_host(db)) if from_numpy else (evm, db)
+
+
+def estimate_timing_offset_from_phase_slope(h_used):
+    """Residual timing from the linear phase slope of an LS channel (core.py:443-469): unwrap
+    angle(h) over the centred subcarriers of NUM_ACTIVE_SUBCARRIERS (read at call time), fit a
+    line, return (slope_rad_per_bin, -slope * N_FFT / (2 pi)); (0.0, 0.0) for an empty h."""
+    dev = _lib.require_gpu()
+    t, from_numpy, nd = _rows(h_used, dev)
+    B, n = t.shape
+    if n == 0:
+        return 0.0, 0.0
+    k = centered_subcarrier_indices(NUM_ACTIVE_SUBCARRIERS)
+    if k.size != n:
+        raise ValueError(f"operands could not be broadcast together with shapes ({k.size},) ({n},)")
+    kb = torch.as_tensor(k.astype(np.int32)).to(dev)
+    slope = torch.empty((B,), dtype=torch.float64, device=dev)
+    sto = torch.empty((B,), dtype=torch.float64, device=dev)
+    _lib.check(_lib.lib().ofs_phase_slope(t.data_ptr(), B, n, kb.data_ptr(), int(N_FFT), slope.data_ptr(),
+                                          sto.data_ptr(), _lib.stream_ptr()), "ofs_phase_slope")
+    if nd == 1:
+        return float(slope[0].item()), float(sto[0].item())
+    return (_lib.to_host(slope), _lib.to_host(sto)) if from_numpy else (slope, sto)

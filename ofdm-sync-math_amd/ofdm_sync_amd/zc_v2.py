@@ -90,6 +90,16 @@ class ZCDetectionResult:
     state: ZCDetectionState
 
 
+def _ref_key(reference) -> tuple:
+    """Cheap identity of a reference for the plan cache, without a device-to-host copy: the
+    content digest of a host array, or (pointer, version counter, size) of a device tensor."""
+    if isinstance(reference, torch.Tensor):
+        return ("dev", reference.data_ptr(), reference._version, reference.numel(), str(reference.dtype))
+    import hashlib
+    r = np.ascontiguousarray(np.asarray(reference, dtype=np.complex128))
+    return ("host", hashlib.sha1(r.tobytes()).hexdigest(), r.size)
+
+
 def _ref_dev(reference, dev):
     r = reference
     if isinstance(r, torch.Tensor):
@@ -102,10 +112,15 @@ def _ref_dev(reference, dev):
 
 class MFPlan:
     """FFT overlap-save matched-filter plan (ofs_zc_mf_plan_create) for one reference and one
-    batch shape [B, n_branch, T]; owns the rocFFT plans, the reference spectrum and scratch."""
+    batch shape [B, n_branch, T]: the rocFFT plans, the reference spectrum and the plan's rocFFT
+    execution info.  The per-call scratch (the blocks' spectra) and rocFFT work buffer are NOT
+    part of the plan: ``run`` takes them from torch's stream-ordered caching allocator, so calls
+    on different streams never share a buffer.  ``run`` holds the plan's lock while it sets the
+    execution info's stream / work buffer and enqueues (the C plan is one caller at a time)."""
 
     def __init__(self, reference, B: int, nb: int, T: int, dev, M: int = 0):
         import ctypes
+        import threading
         r = np.ascontiguousarray(np.asarray(reference.cpu().numpy() if isinstance(reference, torch.Tensor)
                                             else reference, dtype=np.complex128))
         self._lib = _lib.lib()
@@ -114,9 +129,19 @@ class MFPlan:
                                                   ctypes.byref(h), ctypes.byref(wb), ctypes.byref(sb)),
                    "ofs_zc_mf_plan_create")
         self.handle = h.value
-        self.key = (r.tobytes(), int(B), int(nb), int(T), int(M), str(dev))
-        self.scratch = torch.empty((max(int(sb.value), 1),), dtype=torch.uint8, device=dev)
-        self.work = torch.empty((int(wb.value),), dtype=torch.uint8, device=dev) if wb.value else None
+        self.shape = (int(B), int(nb), int(T))
+        self.scratch_bytes, self.work_bytes = max(int(sb.value), 1), int(wb.value)
+        self.device = dev
+        self._lock = threading.Lock()
+
+    def run(self, batch, energy: float, mode: int, corr, mag) -> None:
+        scratch = torch.empty((self.scratch_bytes,), dtype=torch.uint8, device=self.device)
+        work = torch.empty((self.work_bytes,), dtype=torch.uint8, device=self.device) if self.work_bytes else None
+        with self._lock:
+            rc = self._lib.ofs_zc_correlate_fft(self.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
+                                                batch.T, energy, int(mode), _lib.ptr(corr), _lib.ptr(mag),
+                                                scratch.data_ptr(), _lib.ptr(work), _lib.stream_ptr())
+        _lib.check(rc, "ofs_zc_correlate_fft")
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
@@ -126,25 +151,36 @@ class MFPlan:
 
 _mf_plans: dict = {}
 FFT_MIN_TAPS = 256          # the FFT path from this reference length on (direct sums below)
+_NO_PLAN = object()         # cached "this shape has no FFT plan" (OFS_ETOOLONG)
 
 
-def _mf_plan(reference, B, nb, T, dev) -> MFPlan:
-    r = np.asarray(reference.cpu().numpy() if isinstance(reference, torch.Tensor) else reference, np.complex128)
-    key = (r.tobytes(), int(B), int(nb), int(T), 0, str(dev))
-    p = _mf_plans.get(key)
+def _mf_plan(reference, key, B, nb, T, dev):
+    """The cached plan for (reference, shape, device), or None when the overlap-save extract
+    cannot hold this shape's per-block energy prefixes in LDS (OFS_ETOOLONG: many branches or
+    long references).  Plans hold no per-call buffers, so the cache pins only rocFFT plans."""
+    k = (key, int(B), int(nb), int(T), str(dev))
+    p = _mf_plans.get(k)
     if p is None:
-        if len(_mf_plans) >= 4:
+        if len(_mf_plans) >= 8:
             _mf_plans.clear()
-        p = _mf_plans[key] = MFPlan(r, B, nb, T, dev)
-    return p
+        try:
+            p = MFPlan(reference, B, nb, T, dev)
+        except RuntimeError as e:
+            if "status -2)" not in str(e):                 # only OFS_ETOOLONG means "no plan"
+                raise
+            p = _NO_PLAN
+        _mf_plans[k] = p
+    return None if p is _NO_PLAN else p
 
 
 def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, want_mag=False, method: str = "auto"):
     """Correlation of x[B, n_branch, T] with `reference` -> (corr, corr_mag) device tensors.
 
     method "direct": ofs_zc_correlate (O(N) MACs per output, fp64); "fft": ofs_zc_correlate_fft
-    (overlap-save through rocFFT, fp64); "auto": the FFT path for references of >= FFT_MIN_TAPS
-    taps (measured 2048 taps: DESIGN.md §4.5b) in every mode but OFS_ZC_NORMALIZE."""
+    (overlap-save through rocFFT, fp64; raises if the shape has no plan); "auto": the FFT path
+    for references of >= FFT_MIN_TAPS taps (measured 2048 taps: DESIGN.md §4.5b) in every mode
+    but OFS_ZC_NORMALIZE, falling back to the direct sums for shapes the overlap-save extract
+    cannot hold (ofs_zc_mf_plan_create -> OFS_ETOOLONG: e.g. 4 branches at N = 2048)."""
     batch = _lib.as_batch(x, batched=True)
     dev = batch.data.device
     ref, energy = _ref_dev(reference, dev)
@@ -158,12 +194,13 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     use_fft = mode != OFS_ZC_NORMALIZE and batch.B > 0 and batch.T > 0 and (
         method == "fft" or (method == "auto" and N >= FFT_MIN_TAPS))
     if use_fft:
-        plan = _mf_plan(ref, batch.B, batch.nb, batch.T, dev)
-        rc = _lib.lib().ofs_zc_correlate_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
-                                             batch.T, energy, int(mode), _lib.ptr(corr), _lib.ptr(mag),
-                                             plan.scratch.data_ptr(), _lib.ptr(plan.work), _lib.stream_ptr())
-        _lib.check(rc, "ofs_zc_correlate_fft")
-        return corr, mag
+        plan = _mf_plan(reference, _ref_key(reference), batch.B, batch.nb, batch.T, dev)
+        if plan is not None:
+            plan.run(batch, energy, mode, corr, mag)
+            return corr, mag
+        if method == "fft":
+            raise RuntimeError(f"ofs_zc_mf_plan_create: no overlap-save plan for {batch.nb} branches x "
+                               f"{N} taps (extract LDS); use method='direct' (status -2)")
     ci = None
     if mode == OFS_ZC_NORMALIZE:
         ci = torch.as_tensor(corr_in).to(device=dev, dtype=torch.complex128).reshape(batch.B, nout).contiguous()

@@ -351,3 +351,278 @@ int oracle_max_threads(void) {
     return 1;
 #endif
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Full-batch checkers of the fp32 fast paths (cfg4, cfg5): the reference's fp64 values are
+ * recomputed here per stream and the engine's fp32 outputs compared against them under a stated
+ * error model, without materialising fp64 copies of multi-GB outputs.  Per-stream statistics
+ * out; the tests assert on them.  Error-model constants come from the caller (the test states
+ * and justifies them).
+ * ------------------------------------------------------------------------------------------ */
+typedef long double ld;
+
+static inline void ld_cjmul(const double* x, const double* y, ld* re, ld* im) {
+    /* x · conj(y) */
+    *re = (ld)x[0] * y[0] + (ld)x[1] * y[1];
+    *im = (ld)x[1] * y[0] - (ld)x[0] * y[1];
+}
+
+/* combined_sc_min.schmidl_cox_streaming_metric (combined_sc_min.py:116-164): half = N/2,
+ *   P(d) = Σ_br Σ_{k<half} x[d+k]·conj(x[d+half+k]), R(d) = Σ_br Σ_{k<N} |x[d+k]|²,
+ *   M = |P|² / max(R, 1e-12)²;
+ * combined_sc_min.minn_streaming_metric (:60-113, = minn.py:59-112): Q = N/4,
+ *   P(d) = Σ_br [Σ_{k<Q} q0·conj(q1) + Σ_{k<Q} q2·conj(q3)], R(d) = Σ_br Σ |q1|²+|q2|²+|q3|²,
+ *   M = max(Re P, 0)² / max(R, 1e-12)²;   d in [0, T - N].
+ * The window sums are long-double prefix differences (64-bit mantissa: below 1e-18 of a window's
+ * absolute sum for these lengths) - the reference's direct sums to far below fp32 resolution.
+ * Alongside each P, S = Σ |x[i]|·|x[i+lag]| over the same terms (the absolute sum of the error
+ * model).  Output o[8][n_out]: Pc re, Pc im, Rc, Sc, Pm re, Pm im, Rm, Sm. */
+static void scm_ref_one(const double* x, int64_t nb, int64_t T, int64_t N, ld* pre, double* o) {
+    const int64_t half = N / 2, Q = N / 4, nout = T - N + 1;
+    ld* aH = pre;                 /* prefix of x[i]·conj(x[i+half]) (re, im), |.|, lag half  */
+    ld* aQ = pre + 3 * (T + 1);   /* prefix of x[i]·conj(x[i+Q]) (re, im), |.|, lag Q        */
+    ld* eP = pre + 6 * (T + 1);   /* prefix of |x[i]|²                                        */
+    for (int64_t d = 0; d < 8 * nout; ++d) o[d] = 0.0;
+    for (int64_t br = 0; br < nb; ++br) {
+        const double* xs = x + 2 * br * T;
+        ld sh[3] = {0, 0, 0}, sq[3] = {0, 0, 0}, se = 0;
+        for (int64_t i = 0; i <= T; ++i) {
+            aH[3 * i] = sh[0]; aH[3 * i + 1] = sh[1]; aH[3 * i + 2] = sh[2];
+            aQ[3 * i] = sq[0]; aQ[3 * i + 1] = sq[1]; aQ[3 * i + 2] = sq[2];
+            eP[i] = se;
+            if (i == T) break;
+            const double* xi = xs + 2 * i;
+            se += (ld)xi[0] * xi[0] + (ld)xi[1] * xi[1];
+            const ld ax = sqrtl((ld)xi[0] * xi[0] + (ld)xi[1] * xi[1]);
+            if (i + half < T) {
+                ld r, m;
+                const double* y = xs + 2 * (i + half);
+                ld_cjmul(xi, y, &r, &m);
+                sh[0] += r; sh[1] += m; sh[2] += ax * sqrtl((ld)y[0] * y[0] + (ld)y[1] * y[1]);
+            }
+            if (i + Q < T) {
+                ld r, m;
+                const double* y = xs + 2 * (i + Q);
+                ld_cjmul(xi, y, &r, &m);
+                sq[0] += r; sq[1] += m; sq[2] += ax * sqrtl((ld)y[0] * y[0] + (ld)y[1] * y[1]);
+            }
+        }
+        for (int64_t d = 0; d < nout; ++d) {
+            double* od = o;
+            od[0 * nout + d] += (double)(aH[3 * (d + half)] - aH[3 * d]);
+            od[1 * nout + d] += (double)(aH[3 * (d + half) + 1] - aH[3 * d + 1]);
+            od[2 * nout + d] += (double)(eP[d + N] - eP[d]);
+            od[3 * nout + d] += (double)(aH[3 * (d + half) + 2] - aH[3 * d + 2]);
+            const int64_t a0 = d, a1 = d + Q, a2 = d + 2 * Q, a3 = d + 3 * Q;
+            od[4 * nout + d] += (double)((aQ[3 * a1] - aQ[3 * a0]) + (aQ[3 * a3] - aQ[3 * a2]));
+            od[5 * nout + d] += (double)((aQ[3 * a1 + 1] - aQ[3 * a0 + 1]) + (aQ[3 * a3 + 1] - aQ[3 * a2 + 1]));
+            od[6 * nout + d] += (double)(eP[d + N] - eP[d + Q]);
+            od[7 * nout + d] += (double)((aQ[3 * a1 + 2] - aQ[3 * a0 + 2]) + (aQ[3 * a3 + 2] - aQ[3 * a2 + 2]));
+        }
+    }
+}
+
+/* Error model of one window metric (u = 2^-24, the fp32 unit roundoff), oracle values P, R, S:
+ *   |ΔP| <= kP·u·S + u·|P|      |ΔR| <= kR·u·R
+ *   |ΔM| <= 2·(c/R)·(bP/R) + (bP/R)² + 2·M·(bR/R) + kM·u·M       (c = |P| or max(Re P, 0))
+ * i.e. first-order propagation of the P and R errors through M = c²/R² plus the metric's own
+ * fp32 operations. */
+static inline double fp32_metric_bound(double c, double R, double M, double bP, double bR, double kM) {
+    const double Rm = R > 1e-12 ? R : 1e-12;
+    const double p = bP / Rm;
+    return 2.0 * (c / Rm) * p + p * p + 2.0 * M * (bR / Rm) + kM * 0x1p-24 * M + 1e-300;
+}
+
+/* x: [B][nb][T] complex (c64 or c128).  Engine outputs [B][T-N+1]: Mc, Pc (c64), Rc (combined
+ * S&C) and Mm, Pm, Rm (Minn), fp32.  stats [B][8]:
+ *   0 max|ΔMc|   1 max |ΔMc|/bound   2 max |ΔPc|/boundP   3 max |ΔRc|/boundR
+ *   4 max |ΔMm|/max(1, Mm)   5 max |ΔMm|/bound   6 max |ΔPm|/boundP   7 max |ΔRm|/boundR */
+int oracle_sc_minn_check(const void* x, int is_c128, int64_t B, int64_t nb, int64_t T, int64_t N,
+                         const float* Mc, const float* Pc, const float* Rc, const float* Mm, const float* Pm,
+                         const float* Rm, double kP, double kR, double kM, double* stats, int nthreads) {
+    if (!x || B < 0 || nb < 1 || N < 4 || N % 4 || T < N || !Mc || !Pc || !Rc || !Mm || !Pm || !Rm || !stats)
+        return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const int64_t nout = T - N + 1;
+    const double u = 0x1p-24;
+    int rc = 0;
+#pragma omp parallel
+    {
+        ld* pre = (ld*)malloc(sizeof(ld) * 7 * (size_t)(T + 1));
+        double* o = (double*)malloc(sizeof(double) * 8 * (size_t)nout);
+        double* xd = (double*)malloc(sizeof(double) * 2 * (size_t)(nb * T));
+        if (!pre || !o || !xd) {
+#pragma omp atomic write
+            rc = -2;
+        }
+#pragma omp for schedule(dynamic, 8)
+        for (int64_t b = 0; b < B; ++b) {
+            if (!pre || !o || !xd) continue;
+            for (int64_t i = 0; i < 2 * nb * T; ++i)
+                xd[i] = is_c128 ? ((const double*)x)[2 * b * nb * T + i] : (double)((const float*)x)[2 * b * nb * T + i];
+            scm_ref_one(xd, nb, T, N, pre, o);
+            double st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int64_t d = 0; d < nout; ++d) {
+                const int64_t g = b * nout + d;
+                /* combined S&C */
+                {
+                    const double pr = o[d], pi = o[nout + d], R = o[2 * nout + d], S = o[3 * nout + d];
+                    const double ap = hypot(pr, pi), Rm_ = R > 1e-12 ? R : 1e-12, M = ap * ap / (Rm_ * Rm_);
+                    const double bP = kP * u * S + u * ap, bR = kR * u * R;
+                    const double dP = hypot((double)Pc[2 * g] - pr, (double)Pc[2 * g + 1] - pi);
+                    const double dR = fabs((double)Rc[g] - R), dM = fabs((double)Mc[g] - M);
+                    const double bM = fp32_metric_bound(ap, R, M, bP, bR, kM);
+                    if (!(dM <= st[0])) st[0] = dM;                     /* NaN propagates as a failure */
+                    if (!(dM / bM <= st[1])) st[1] = dM / bM;
+                    if (!(dP / (bP + 1e-300) <= st[2])) st[2] = dP / (bP + 1e-300);
+                    if (!(dR / (bR + 1e-300) <= st[3])) st[3] = dR / (bR + 1e-300);
+                }
+                /* Minn */
+                {
+                    const double pr = o[4 * nout + d], pi = o[5 * nout + d], R = o[6 * nout + d], S = o[7 * nout + d];
+                    const double c = pr > 0.0 ? pr : 0.0, Rm_ = R > 1e-12 ? R : 1e-12, M = c * c / (Rm_ * Rm_);
+                    const double bP = kP * u * S + u * hypot(pr, pi), bR = kR * u * R;
+                    const double dP = hypot((double)Pm[2 * g] - pr, (double)Pm[2 * g + 1] - pi);
+                    const double dR = fabs((double)Rm[g] - R), dM = fabs((double)Mm[g] - M);
+                    const double bM = fp32_metric_bound(c, R, M, bP, bR, kM);
+                    const double rn = dM / (M > 1.0 ? M : 1.0);
+                    if (!(rn <= st[4])) st[4] = rn;
+                    if (!(dM / bM <= st[5])) st[5] = dM / bM;
+                    if (!(dP / (bP + 1e-300) <= st[6])) st[6] = dP / (bP + 1e-300);
+                    if (!(dR / (bR + 1e-300) <= st[7])) st[7] = dR / (bR + 1e-300);
+                }
+            }
+            for (int k = 0; k < 8; ++k) stats[8 * b + k] = st[k];
+        }
+        free(pre); free(o); free(xd);
+    }
+    return rc;
+}
+
+/* In-place iterative radix-2 DIT FFT (fp64), N a power of two; tw[k] = exp(-2πi·k/N), k < N/2,
+ * from libm cos/sin of exact index ratios.  Normwise relative error ~log2(N)·1e-16. */
+static void fft_pow2(double* a, int64_t N, const double* tw) {
+    for (int64_t i = 1, j = 0; i < N; ++i) {
+        int64_t bit = N >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            double t0 = a[2 * i], t1 = a[2 * i + 1];
+            a[2 * i] = a[2 * j]; a[2 * i + 1] = a[2 * j + 1];
+            a[2 * j] = t0; a[2 * j + 1] = t1;
+        }
+    }
+    for (int64_t len = 2; len <= N; len <<= 1) {
+        const int64_t h = len >> 1, step = N / len;
+        for (int64_t s0 = 0; s0 < N; s0 += len) {
+            for (int64_t k = 0; k < h; ++k) {
+                const double wr = tw[2 * k * step], wi = tw[2 * k * step + 1];
+                double* p = a + 2 * (s0 + k);
+                double* q = a + 2 * (s0 + k + h);
+                const double vr = q[0] * wr - q[1] * wi, vi = q[0] * wi + q[1] * wr;
+                q[0] = p[0] - vr; q[1] = p[1] - vi;
+                p[0] += vr; p[1] += vi;
+            }
+        }
+    }
+}
+
+/* zc_freq.compute_frequency_metric (zc_freq.py:62-99) at every offset off in [0, T-(N+cp)]:
+ *   window w = x[br][off+cp : off+cp+N];  b_j = fftshift(fft(w))[(N/2 + idx_j) % N] = DFT_N(w) at
+ *   frequency idx_j mod N;  metric = |Σ_br Σ_j conj(t_j)·b_j|² / max(E_t·Σ_br Σ_j |b_j|², 1e-12).
+ * The window's DFT in fp64: a radix-2 FFT for N a power of two (the reference's np.fft.fft), else a
+ * direct DFT of the bins; twiddles from libm of exact index ratios.  Engine metric [B][noff] (fp32 if
+ * is_f32 else fp64).  Error model of an fp32 FFT-based engine (eps = its normwise relative FFT error):
+ *   ρ = ||Δb||/||b|| <= eps·sqrt(N)·||w||/||b||   (Parseval: ||ΔX|| <= eps·||X|| = eps·sqrt(N)·||w||)
+ *   |Δm| <= 2·(sqrt(nb·m) + m)·ρ + (nb + 1)·ρ² + kM·u·m
+ * (first-order perturbation of m = |<T, b>|² / (E_t·||b||²) over the nb·62 gathered bins, plus the
+ * metric's own fp32 operations).  stats [B][3]: 0 max|Δm|, 1 max |Δm|/bound, 2 max oracle metric. */
+int oracle_zc_freq_check(const void* x, int is_c128, int64_t B, int64_t nb, int64_t T, int64_t N, int64_t cp,
+                         int32_t nbins, const int32_t* idx, const double* tmpl, double tmpl_energy,
+                         const void* eng, int is_f32, double eps, double kM, double* stats, int nthreads) {
+    if (!x || B < 0 || nb < 1 || N < 2 || cp < 0 || T < N + cp || nbins < 1 || !idx || !tmpl || !eng || !stats)
+        return -1;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+    const int64_t noff = T - (N + cp) + 1;
+    const int pow2 = (N & (N - 1)) == 0;
+    double* tw = (double*)malloc(sizeof(double) * (pow2 ? (size_t)N : 2 * (size_t)nbins * (size_t)N));
+    if (!tw) return -2;
+    if (pow2) {
+        for (int64_t k = 0; k < N / 2; ++k) {
+            const double a = -2.0 * M_PI * (double)k / (double)N;
+            tw[2 * k] = cos(a);
+            tw[2 * k + 1] = sin(a);
+        }
+    } else {
+        for (int j = 0; j < nbins; ++j) {
+            const int64_t k = ((int64_t)idx[j] % N + N) % N;
+            for (int64_t n = 0; n < N; ++n) {
+                const double a = -2.0 * M_PI * (double)((k * n) % N) / (double)N;
+                tw[2 * ((int64_t)j * N + n)] = cos(a);
+                tw[2 * ((int64_t)j * N + n) + 1] = sin(a);
+            }
+        }
+    }
+    int rc = 0;
+#pragma omp parallel
+    {
+        double* w = (double*)malloc(sizeof(double) * 2 * (size_t)N);
+        if (!w) {
+#pragma omp atomic write
+            rc = -2;
+        }
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t b = 0; b < B; ++b) {
+            if (!w) continue;
+            double st[3] = {0, 0, 0};
+            for (int64_t off = 0; off < noff; ++off) {
+                double sr = 0, si = 0, D = 0, W2 = 0;
+                for (int64_t br = 0; br < nb; ++br) {
+                    const int64_t base = (b * nb + br) * T + off + cp;
+                    for (int64_t n = 0; n < N; ++n) {
+                        w[2 * n] = is_c128 ? ((const double*)x)[2 * (base + n)] : (double)((const float*)x)[2 * (base + n)];
+                        w[2 * n + 1] = is_c128 ? ((const double*)x)[2 * (base + n) + 1]
+                                               : (double)((const float*)x)[2 * (base + n) + 1];
+                        W2 += w[2 * n] * w[2 * n] + w[2 * n + 1] * w[2 * n + 1];
+                    }
+                    if (pow2) fft_pow2(w, N, tw);
+                    for (int j = 0; j < nbins; ++j) {
+                        double br_ = 0, bi_ = 0;
+                        if (pow2) {
+                            const int64_t k = ((int64_t)idx[j] % N + N) % N;
+                            br_ = w[2 * k]; bi_ = w[2 * k + 1];
+                        } else {
+                            const double* t = tw + 2 * (int64_t)j * N;
+                            for (int64_t n = 0; n < N; ++n) {
+                                br_ += w[2 * n] * t[2 * n] - w[2 * n + 1] * t[2 * n + 1];
+                                bi_ += w[2 * n] * t[2 * n + 1] + w[2 * n + 1] * t[2 * n];
+                            }
+                        }
+                        /* conj(t_j)·b_j  (np.vdot conjugates its first argument, zc_freq.py:95) */
+                        sr += tmpl[2 * j] * br_ + tmpl[2 * j + 1] * bi_;
+                        si += tmpl[2 * j] * bi_ - tmpl[2 * j + 1] * br_;
+                        D += br_ * br_ + bi_ * bi_;
+                    }
+                }
+                const double den = tmpl_energy * D;
+                const double m = (sr * sr + si * si) / (den > 1e-12 ? den : 1e-12);
+                const double e = is_f32 ? (double)((const float*)eng)[b * noff + off] : ((const double*)eng)[b * noff + off];
+                const double dm = fabs(e - m);
+                const double rho = D > 0 ? eps * sqrt((double)N) * sqrt(W2) / sqrt(D) : INFINITY;
+                const double bound = 2.0 * (sqrt((double)nb * m) + m) * rho + (double)(nb + 1) * rho * rho +
+                                     kM * 0x1p-24 * m + 1e-300;
+                if (!(dm <= st[0])) st[0] = dm;
+                if (!(dm / bound <= st[1])) st[1] = dm / bound;
+                if (m > st[2]) st[2] = m;
+            }
+            for (int k = 0; k < 3; ++k) stats[3 * b + k] = st[k];
+        }
+        free(w);
+    }
+    free(tw);
+    return rc;
+}

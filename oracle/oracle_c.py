@@ -29,6 +29,13 @@ def lib():
                                        c_int, c_double, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                        c_void_p, c_void_p, c_int]
         l.oracle_max_threads.restype = c_int
+        l.oracle_sc_minn_check.restype = c_int
+        l.oracle_sc_minn_check.argtypes = [c_void_p, c_int, c_int64, c_int64, c_int64, c_int64] + [c_void_p] * 6 + \
+            [c_double, c_double, c_double, c_void_p, c_int]
+        l.oracle_zc_freq_check.restype = c_int
+        l.oracle_zc_freq_check.argtypes = [c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
+                                           c_void_p, c_void_p, c_double, c_void_p, c_int, c_double, c_double,
+                                           c_void_p, c_int]
         l.oracle_minn_rtl.restype = c_int
         l.oracle_minn_rtl.argtypes = [c_void_p, c_int64, c_int64, c_int64, c_int64, c_int, c_int64, c_int, c_int,
                                       c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -89,6 +96,63 @@ def minn_rtl(x, Q, smooth_shift=3, threshold_value=3276, threshold_frac_bits=15,
         raise RuntimeError(f"oracle_minn_rtl failed ({rc})")
     out.update(events=ev, n_events=n_ev, open_gate_start=og)
     return out
+
+
+def _host(a, dtype):
+    a = np.ascontiguousarray(a)
+    if a.dtype != dtype:
+        raise TypeError(f"expected {dtype}, got {a.dtype}")
+    return a
+
+
+SC_MINN_STATS = ("comb_max_dM", "comb_dM_over_bound", "comb_dP_over_bound", "comb_dR_over_bound",
+                 "minn_max_dM_rel1", "minn_dM_over_bound", "minn_dP_over_bound", "minn_dR_over_bound")
+
+
+def sc_minn_check(x, N, Mc, Pc, Rc, Mm, Pm, Rm, kP, kR, kM, nthreads=0):
+    """Engine fp32 combined S&C + Minn outputs ([B, T-N+1]) against the fp64 reference values of
+    x [B, nb, T] (oracle_sc_minn_check).  Returns the per-stream statistics [B, 8] (SC_MINN_STATS)."""
+    x = np.ascontiguousarray(x)
+    if x.ndim == 2:
+        x = x[:, None, :]
+    if x.dtype not in (np.complex64, np.complex128):
+        raise TypeError("x must be complex64 / complex128")
+    B, nb, T = x.shape
+    f32 = [_host(a, np.float32) for a in (Mc, Rc, Mm, Rm)]
+    c64 = [_host(a, np.complex64) for a in (Pc, Pm)]
+    st = np.zeros((B, 8))
+    rc = lib().oracle_sc_minn_check(x.ctypes.data, int(x.dtype == np.complex128), B, nb, T, int(N),
+                                    f32[0].ctypes.data, c64[0].ctypes.data, f32[1].ctypes.data, f32[2].ctypes.data,
+                                    c64[1].ctypes.data, f32[3].ctypes.data, float(kP), float(kR), float(kM),
+                                    st.ctypes.data, int(nthreads))
+    if rc:
+        raise RuntimeError(f"oracle_sc_minn_check failed ({rc})")
+    return st
+
+
+def zc_freq_check(x, N, cp, idx, tmpl, tmpl_energy, metric, eps, kM, nthreads=0):
+    """Engine zc_freq metric [B, noff] (fp32 or fp64) against the direct-DFT fp64 reference of
+    x [B, nb, T] (oracle_zc_freq_check).  Returns per-stream [B, 3]: max|dm|, max |dm|/bound,
+    max oracle metric."""
+    x = np.ascontiguousarray(x)
+    if x.ndim == 2:
+        x = x[:, None, :]
+    if x.dtype not in (np.complex64, np.complex128):
+        raise TypeError("x must be complex64 / complex128")
+    B, nb, T = x.shape
+    m = np.ascontiguousarray(metric)
+    if m.dtype not in (np.float32, np.float64) or m.shape[0] != B or m.size != B * (T - N - cp + 1):
+        raise ValueError("metric must be [B, T-N-cp+1] float32/float64")
+    idx = np.ascontiguousarray(np.asarray(idx, np.int32))
+    tb = np.ascontiguousarray(np.asarray(tmpl, np.complex128))
+    st = np.zeros((B, 3))
+    rc = lib().oracle_zc_freq_check(x.ctypes.data, int(x.dtype == np.complex128), B, nb, T, int(N), int(cp),
+                                    int(idx.size), idx.ctypes.data, tb.ctypes.data, float(tmpl_energy),
+                                    m.ctypes.data, int(m.dtype == np.float32), float(eps), float(kM),
+                                    st.ctypes.data, int(nthreads))
+    if rc:
+        raise RuntimeError(f"oracle_zc_freq_check failed ({rc})")
+    return st
 
 
 def max_threads() -> int:

@@ -71,9 +71,12 @@ def classify_aa(M_g, n_g, ei_g, er_g, P_o, M_o, n_o, ei_o, er_o, L, threshold=0.
     k = np.arange(E)[None, :]
     live = k < ne[:, None]
     ints_eq = np.all((ei_g[:, :E, :3] == ei_o[:, :E, :3]).all(axis=2) | ~live, axis=1) & same_n
-    ang = lambda r: np.arctan2(r[..., 1], r[..., 0])                               # noqa: E731
-    dang = np.abs(np.angle(np.exp(1j * (ang(er_g[:, :E]) - ang(er_o[:, :E])))))
     peak_eq = (ei_g[:, :E, 0] == ei_o[:, :E, 0]) & live & (k < np.minimum(n_o, E)[:, None])
+    # event slots past n_events are never written by the engine (uninitialised buffers): the
+    # angle is only formed where both sides hold a live event with the same peak
+    rg = np.where(peak_eq[..., None], er_g[:, :E, :2], 1.0)
+    ro = np.where(peak_eq[..., None], er_o[:, :E, :2], 1.0)
+    dang = np.abs(np.angle(np.exp(1j * (np.arctan2(rg[..., 1], rg[..., 0]) - np.arctan2(ro[..., 1], ro[..., 0])))))
     cfo_err = np.where(peak_eq, dang, 0.0)
     exact = ints_eq & ~any_flag
     cls = np.full(B, "exact", dtype=object)

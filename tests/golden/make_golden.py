@@ -17,6 +17,10 @@ Reference entry points exercised (file:line into /root/reference):
   minn_rtl.minn_rtl_streaming_metric  minn_rtl.py:667-733
   minn_rtl.detect_minn_rtl             minn_rtl.py:750-825
   core.estimate_cfo_from_cp            core.py:179-196
+  core.apply_cfo / ofdm_fft_used / ls_channel_estimate / equalize / remove_common_phase /
+  align_complex_gain / evm_rms_db / estimate_timing_offset_from_phase_slope
+                                       core.py:123-138, 171-176, 339-370, 443-469
+  sync_aa.quantize_adc                 sync_aa.py:263-291
   park.park_streaming_metric           park.py:64-114     (park.N_FFT overridden per case)
   zc_freq.compute_frequency_metric     zc_freq.py:62-99   (zc_freq.N_FFT / CYCLIC_PREFIX overridden)
   zc_v2.matched_filter_correlation / normalize_correlation / zc_streaming_detection /
@@ -299,6 +303,51 @@ def gen_backend(R, cases):
                            slope=np.float64(slope), sto=np.float64(sto), y_pilot=y_p)
 
 
+def gen_backend_ops(R, cases):
+    """The back-end helpers one by one, as sc.run_simulation calls them (sc.py:274-311), plus
+    core.apply_cfo and sync_aa.quantize_adc: inputs and the reference's outputs per helper."""
+    core, ch, sa = R["core"], R["channel"], R["sync_aa"]
+    N, CP, fs = core.N_FFT, core.CYCLIC_PREFIX, core.SAMPLE_RATE_HZ
+    for name, seed, snr, cir, cfo, shift in (("bops_cir1_2br", 31, 12.0, "cir1", 1500.0, 2),
+                                             ("bops_awgn_1br", 32, 25.0, None, -800.0, 0)):
+        rng = np.random.default_rng(seed)
+        pil, pil_used = core.build_random_qpsk_symbol(rng, include_cp=True)
+        dat, dat_used = core.build_random_qpsk_symbol(rng, include_cp=True)
+        pad = 400
+        tx = np.concatenate([np.zeros(pad, complex), pil, dat, np.zeros(200, complex)])
+        rx = ch.apply_channel(tx, snr, rng, None if cir is None else ch.load_measured_cir(cir)[:2])
+        rx_cfo = core.apply_cfo(rx, cfo, fs)                               # core.py:123-138 (1-D or 2-D)
+        rx1_cfo = core.apply_cfo(np.atleast_2d(rx)[0], -cfo / 3, fs)
+        ps = pad + shift
+        ds = ps + CP + N
+        eff = np.mean(np.atleast_2d(core.apply_cfo(rx_cfo, -cfo, fs)), axis=0)
+        sym_p, sym_d = eff[ps + CP:ps + CP + N], eff[ds + CP:ds + CP + N]
+        y_p = core.ofdm_fft_used(sym_p)                                   # core.py:171-176
+        y_short = core.ofdm_fft_used(sym_p[:N - 300])                     # fft(x, n=N) zero-pads
+        y_long = core.ofdm_fft_used(eff[ps:ps + N + 200])                 # ... and truncates
+        h = core.ls_channel_estimate(y_p, pil_used)                       # :339-341
+        y_d = core.ofdm_fft_used(sym_d)
+        xhat = core.equalize(y_d, h)                                      # :344-345
+        x_cpe, cpe = core.remove_common_phase(xhat)                       # :348-354, mean angle
+        x_cpe_ref, cpe_ref = core.remove_common_phase(xhat, dat_used)     # ... against a reference
+        xa, gain = core.align_complex_gain(xhat, dat_used)                # :357-362
+        evm, evm_db = core.evm_rms_db(xa, dat_used)                       # :365-370
+        slope, sto = core.estimate_timing_offset_from_phase_slope(h)      # :443-469
+        rms = float(np.sqrt(np.mean(np.abs(np.atleast_2d(rx_cfo)[0]) ** 2)))
+        q64 = sa.quantize_adc(np.atleast_2d(rx_cfo)[0], 4.0 * rms)                         # sync_aa.py:263-291
+        q64_np = sa.quantize_adc(np.atleast_2d(rx_cfo)[0], np.float64(2.5 * rms), bits=8)  # numpy scalar
+        x32 = np.atleast_2d(rx_cfo)[0].astype(np.complex64)
+        q32 = sa.quantize_adc(x32, 3.0 * rms)                                              # fp32 (weak scalar)
+        q32_np = sa.quantize_adc(x32, np.float64(3.0 * rms))                              # promotes to fp64
+        cases[name] = dict(kind="backend_ops", rx=rx, cfo=np.float64(cfo), fs=np.float64(fs), rx_cfo=rx_cfo,
+                           rx1_cfo=rx1_cfo, sym_p=sym_p, sym_d=sym_d, y_p=y_p, y_short=y_short, y_long=y_long,
+                           pil_used=pil_used, dat_used=dat_used, h=h, y_d=y_d, xhat=xhat, x_cpe=x_cpe,
+                           cpe=np.float64(cpe), x_cpe_ref=x_cpe_ref, cpe_ref=np.float64(cpe_ref), xa=xa,
+                           gain=np.complex128(gain), evm=np.float64(evm), evm_db=np.float64(evm_db),
+                           slope=np.float64(slope), sto=np.float64(sto), rms=np.float64(rms), q64=q64,
+                           q64_np=q64_np, x32=x32, q32=q32, q32_np=q32_np)
+
+
 def gen_park(R, cases):
     pk = R["park"]
     core = R["core"]
@@ -497,6 +546,7 @@ def main():
     gen_minn_rtl(R, cases)
     gen_cp_cfo(R, cases)
     gen_backend(R, cases)
+    gen_backend_ops(R, cases)
     gen_park(R, cases)
     gen_zc(R, cases)
     gen_post(R, cases)

@@ -2,7 +2,9 @@
 P/R/M/valid not requested the kernels skip those stores and keep the events on chip.  The
 events must be identical to the ones of the full call on every dispatch plan (fp32 fast path,
 int12 integer-exact path, general engine with fused events); the general engine's multi-tile
-plan still gets P/M buffers from the mirror.  Exact equality: same kernel, same arithmetic."""
+plan still gets P/M buffers from the mirror.  Exact equality: same kernel, same arithmetic (the
+register-staged fp32 detect-only kernel runs 8 samples per lane per row, aa_fast.hip pick_e_do, so
+its full call is compared at that row width: OFS_FAST_E=8)."""
 import numpy as np
 import pytest
 
@@ -32,13 +34,16 @@ def _batch(kind, B, T, L):
                                                        ("c128", 3000, 256, 3000, 4000), ("c128", 9000, 512, 3000, 4000),
                                                        ("c64", 4096, 512, 1100, 1200), ("c64", 5315, 256, 1100, 1200),
                                                        ("c64", 9000, 100, 2, 2)])
-def test_detect_only_events_equal_full(kind, T, L, plan_lo, plan_hi):
+def test_detect_only_events_equal_full(kind, T, L, plan_lo, plan_hi, monkeypatch):
     B = 512
     x = _batch(kind, B, T, L)
     b = _lib.as_batch(x, batched=True)
     plan = _lib.lib().ofs_aa_plan(b.fmt, _lib.resolve_precision(b, None), 1, T, L)
     assert plan_lo <= plan <= plan_hi
+    if 1000 <= plan < 1100:                        # register-staged fp32 kernel: DO row width
+        monkeypatch.setenv("OFS_FAST_E", "8")
     full = sync_aa.aa_detect_streaming_batched(x, L)
+    monkeypatch.delenv("OFS_FAST_E", raising=False)
     det = sync_aa.aa_detect_streaming_batched(x, L, outputs=())
     assert det.P is None and det.M is None and det.R is None
     assert torch.equal(full.n_events, det.n_events)

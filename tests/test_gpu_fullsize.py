@@ -8,13 +8,17 @@ size-independent properties plus oracle parity on sampled streams.
   cfg3  detect-only (events without P/R/M) on the full 65536 x 1024 batch: every stream's events
         against the C oracle under oracle/parity.py's stated near-tie criterion;
   cfg4  32768 x 4096 c64 (one GPU's shard of 262144), fused combined S&C + Minn, N = 2048:
-        oracle on 512 streams (M 1e-6), combined S&C M <= 1/4 and Minn M >= 0 on every stream;
-  cfg5  the full 1M x 4096 c64 batch (32 GiB), zc_freq fp32 window FFT: oracle on 4096 sequences
-        (2e-5 abs), 0 <= metric <= 1 on every sequence.
+        EVERY stream and output against the C oracle's fp64 values (oracle_sc_minn_check): M, P,
+        R within the fp32 error model of tests/error_models.py (model 1), combined S&C M within
+        the north-star 1e-6 absolute, Minn M within 1e-6·max(1, M);
+  cfg5  the full 1M x 4096 c64 batch (32 GiB), zc_freq fp32 window FFT: EVERY sequence against
+        the C oracle's fp64 FFT (oracle_zc_freq_check) within error model 2.
+Each test prints the measured maximum error and its ratio to the bound.
 """
 import numpy as np
 import pytest
 
+import error_models as EM
 import ofdm_oracle as O
 import oracle_c
 
@@ -90,31 +94,43 @@ def test_cfg2_minn_rtl_full_batch_exact(monkeypatch):
         assert np.array_equal(ev[b, :k], o["events"][b, :k])
 
 
-def test_cfg4_fused_shard_full_size():
+def test_cfg4_fused_shard_every_stream_vs_oracle():
     B, T, N = 32768, 4096, 2048
     x = synth.make_aa_batch(B, T, N // 2, seed=4, device="cuda")
+    assert _lib.lib().ofs_win_plan(4, _lib.C64, _lib.FP32, 1, T, N) == 42        # sc_minn kernel, E = 4
     (Mm, Pm, Rm), (Ms, Ps, Rs) = combined_sc_min.sc_minn_streaming_metrics_batched(x, N)
     assert Ms.shape == (B, T - N + 1)
-    assert bool(torch.isfinite(Ms).all()) and bool(torch.isfinite(Mm).all())
-    assert float(Ms.max()) <= 0.25 + 1e-6 and float(Mm.min()) >= 0.0       # |P| <= (E1+E2)/2
-    xh = x[:: B // 512].cpu().numpy().astype(np.complex128)
-    for i, b in enumerate(range(0, B, B // 512)):
-        Mo, Po, Ro = O.comb_sc_metric(xh[i], N)
-        assert np.max(np.abs(Ms[b].cpu().numpy() - Mo)) < 1e-6
-        Mo, Po, Ro = O.minn_metric(xh[i], N)
-        mm = Mm[b].cpu().numpy()
-        assert np.all(np.abs(mm - Mo) <= 1e-6 * np.maximum(1.0, np.abs(Mo)))
+    kP, kR, kM = EM.win_fast_k(4, 1)
+    h = lambda t: t.cpu().numpy()                                                 # noqa: E731
+    st = np.concatenate([oracle_c.sc_minn_check(h(x[lo:lo + 4096]), N, h(Ms[lo:lo + 4096]), h(Ps[lo:lo + 4096]),
+                                                h(Rs[lo:lo + 4096]), h(Mm[lo:lo + 4096]), h(Pm[lo:lo + 4096]),
+                                                h(Rm[lo:lo + 4096]), kP, kR, kM, nthreads=16)
+                         for lo in range(0, B, 4096)])
+    worst = dict(zip(oracle_c.SC_MINN_STATS, st.max(axis=0)))
+    print("cfg4 every stream:", {k: float(f"{v:.3g}") for k, v in worst.items()})
+    assert not np.isnan(st).any()
+    assert worst["comb_max_dM"] <= 1e-6 and worst["minn_max_dM_rel1"] <= 1e-6          # north star
+    for k in ("comb_dM_over_bound", "comb_dP_over_bound", "comb_dR_over_bound", "minn_dM_over_bound",
+              "minn_dP_over_bound", "minn_dR_over_bound"):
+        assert worst[k] <= 1.0, k
 
 
-def test_cfg3_detect_only_full_batch_vs_oracle():
+def test_cfg3_detect_only_full_batch_vs_oracle(monkeypatch):
     """The headline batch with P/R/M not stored (SURVEY §8d detect-only): every stream's events
-    against the C oracle (oracle/parity.py: exact except stated near-ties; CFO angle <= 1e-6)."""
+    against the C oracle (oracle/parity.py: exact except stated near-ties; CFO angle <= 1e-6).
+    The detect-only kernel runs 8 samples per lane per row (aa_fast.hip pick_e_do); the M the
+    classifier needs comes from the storing kernel forced to the same row width, i.e. the same
+    arithmetic, so both calls' events are identical too."""
     import parity
     B, T, L = 65536, 1024, 512
     x = synth.headline_batch(B, T, L, seed=777)
+    monkeypatch.setenv("OFS_FAST_E", "8")
     full = sync_aa.aa_detect_streaming_batched(x, L, outputs=("M",), max_events=8)
+    monkeypatch.delenv("OFS_FAST_E")
     det = sync_aa.aa_detect_streaming_batched(x, L, outputs=(), max_events=8)
     assert torch.equal(full.n_events, det.n_events)
+    k = int(min(det.n_events.max(), 8))
+    assert torch.equal(full.ev_int[:, :k], det.ev_int[:, :k]) and torch.equal(full.ev_real[:, :k], det.ev_real[:, :k])
     o = oracle_c.aa_detect(x.cpu().numpy(), L, max_events=8, nthreads=16)
     r = parity.classify_aa(full.M.cpu().numpy().astype(np.float64), det.n_events.cpu().numpy(),
                            det.ev_int.cpu().numpy(), det.ev_real.cpu().numpy(), o["P"], o["M"], o["n_events"],
@@ -123,7 +139,7 @@ def test_cfg3_detect_only_full_batch_vs_oracle():
     assert r["mismatch"] == 0 and r["cfo_over_tol"] == 0 and r["events_engine"] == r["events_oracle"]
 
 
-def test_cfg5_full_batch():
+def test_cfg5_full_batch_every_sequence_vs_oracle():
     B, N = 1 << 20, 4096
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.empty((B, N), dtype=torch.complex64, device="cuda")
@@ -132,10 +148,16 @@ def test_cfg5_full_batch():
     sym = torch.from_numpy(O.pss_symbol(N).astype(np.complex64)).cuda()
     x[::97] += 4.0 * sym                                                 # some windows carry the PSS
     idx, t, e = O.zc_template()
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, N, N, 0) == 3
     m = zc_freq.compute_frequency_metric_batched(x, idx, t, e, N=N, cp=0)
-    assert m.shape == (B, 1)
-    assert float(m.min()) >= 0.0 and float(m.max()) <= 1.0 + 1e-5        # Cauchy-Schwarz
-    assert float(m[::97].min()) > 0.5
-    for b in list(range(0, B, B // 4096)) + [97, 194, B - 1]:
-        mo = O.zc_freq_metric(x[b].cpu().numpy().astype(np.complex128)[None], N, 0, idx, t, e)
-        assert abs(float(m[b, 0]) - mo[0]) < 2e-5
+    assert m.shape == (B, 1) and m.dtype == torch.float32
+    mh = m.cpu().numpy()
+    assert float(mh[::97].min()) > 0.5
+    eps = EM.zc_win_eps(N)
+    CH = 1 << 16
+    st = np.concatenate([oracle_c.zc_freq_check(x[lo:lo + CH].cpu().numpy(), N, 0, idx, t, e, mh[lo:lo + CH], eps,
+                                                6.0, nthreads=16) for lo in range(0, B, CH)])
+    print(f"cfg5 every sequence: max |dm| = {st[:, 0].max():.3g}, max |dm|/bound = {st[:, 1].max():.3g} "
+          f"(eps = {eps:.3g}), oracle metric max {st[:, 2].max():.3f}")
+    assert not np.isnan(st).any()
+    assert st[:, 1].max() <= 1.0

@@ -133,10 +133,10 @@ def cfg2a(dev, st, steps, warmup, cp12=False):
                 bytes_per_sample=f"{insz} in + P 16 + R 8 + M 8 + valid 1")
 
 
-def cfg2b(dev, st, steps, warmup, cp12=False):
+def cfg2b(dev, st, steps, warmup, cp12=False, B=4096):
     """cfg2 (minn_rtl side): Q=64, int12 I/Q, B=4096 x T=1024, fused IIR + threshold + gate;
-    cp12: packed 12-bit AXIS words."""
-    B, T, Q = 4096, 1024, 64
+    cp12: packed 12-bit AXIS words.  B: batch sweep (``--configs cfg2b@B=65536``)."""
+    T, Q = 1024, 64
     x = int12(synth.make_aa_batch(B, T, 128, seed=9, device=dev))
     if cp12:
         x = packed(x)
@@ -162,7 +162,7 @@ def cfg2b(dev, st, steps, warmup, cp12=False):
     plan = L_.ofs_rtl_plan(fmt, 1, T, Q)
     kernel = (f"rtl_exact_kernel<E={(plan - 2000) // 10},MW={plan % 10}> (integer-exact metric + in-wave "
               "IIR + closed-form gate)" if plan else "win_kernel<CI16,fp64,RTL> + rtl_iir_kernel")
-    return dict(config="cfg2b_cp12" if cp12 else "cfg2b",
+    return dict(config=("cfg2b_cp12" if cp12 else "cfg2b") + ("" if B == 4096 else f"@B={B}"),
                 workload=f"minn_rtl Q={Q}, int12 {'packed AXIS words' if cp12 else 'I/Q'}, {B} x {T}, fp64 + "
                          "sequential IIR/gate",
                 kernel=kernel, samples=B * T, ms=ms, alg_bytes=nbytes,
@@ -546,6 +546,27 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
 "cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
+def _selftest_config(name):
+    """--selftest-cpu stand-in for a config: a rank-dependent sleep per step instead of the HIP
+    launch (rank r sleeps 2·(r+1) ms), host-timed between barriers, same result fields, so the
+    launcher, the strong-scaling shard split, the sums over ranks and MAX-of-times are exercised
+    on CPU (gloo).  Never used without --selftest-cpu."""
+    def run(dev, st, steps, warmup, B=None, n_seq=None, seed=0):
+        n = B if B is not None else (n_seq if n_seq is not None else 4096)
+        delay = 0.002 * (shard.rank_info().rank + 1)
+        for _ in range(warmup):
+            time.sleep(delay)
+        if _DIST is not None:
+            _DIST.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            time.sleep(delay)
+        ms = (time.perf_counter() - t0) * 1e3 / steps
+        return dict(config=name, workload="selftest (sleep)", kernel="none", samples=n * 4096, ms=ms,
+                    alg_bytes=n * 4096 * 8, selftest=True, seed=seed)
+    return run
+
+
 # strong-scaled configs: global batch and the keyword that receives the rank's shard
 SHARDED = {"cfg4": ("cfg4_global", "B"), "cfg5": ("cfg5_global", "n_seq"), "cfg5_rocfft": ("cfg5_global", "n_seq"),
            "cfg5_rocfft_dense": ("cfg5_global", "n_seq"), "cfg5_rocfft_chunked": ("cfg5_global", "n_seq")}
@@ -561,28 +582,38 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--cfg4-global", type=int, default=262144, help="cfg4 streams over all GPUs")
     ap.add_argument("--cfg5-global", type=int, default=1 << 20, help="cfg5 sequences over all GPUs")
+    ap.add_argument("--selftest-cpu", action="store_true",
+                    help="launcher self-test on CPU (gloo, a rank-dependent sleep per config instead of the HIP "
+                         "launch): rank start-up, strong-scaling shards, sums over ranks, MAX-of-times")
     a = ap.parse_args(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.path.insert(0, ROOT)
         import bench
-        return bench.launch_ranks(argparse.Namespace(gpus=a.gpus, selftest_cpu=False), argv,
+        return bench.launch_ranks(argparse.Namespace(gpus=a.gpus, selftest_cpu=a.selftest_cpu), argv,
                                   script=os.path.abspath(__file__))
     info = shard.rank_info()
     if info.world != a.gpus:
         raise SystemExit(f"bench_configs.py: --gpus {a.gpus} but WORLD_SIZE={info.world}")
-    torch.cuda.set_device(info.local_rank)
-    dev = torch.device("cuda", info.local_rank)
-    _DIST = shard.init("nccl", dev)
-    st = torch.cuda.current_stream(dev)
-    for name in a.configs.split(","):
+    if a.selftest_cpu:
+        dev = torch.device("cpu")
+        _DIST = shard.init("gloo")
+        st = None
+    else:
+        torch.cuda.set_device(info.local_rank)
+        dev = torch.device("cuda", info.local_rank)
+        _DIST = shard.init("nccl", dev)
+        st = torch.cuda.current_stream(dev)
+    for spec in a.configs.split(","):
         t0 = time.perf_counter()
-        kw, scale = {}, 1
+        name, _, params = spec.partition("@")           # "cfg2b@B=65536": keyword overrides
+        kw = {k: int(v) for k, v in (p.split("=") for p in params.split(";") if p)}
         if name in SHARDED:
             gkey, arg = SHARDED[name]
             total = getattr(a, gkey)
             lo, hi = shard.shard_bounds(total, info.rank, info.world)
-            kw = {arg: hi - lo, "seed": shard.shard_seed(5, info.rank)}
-        r = CONFIGS[name](dev, st, a.steps, a.warmup, **kw)
+            kw.update({arg: hi - lo, "seed": shard.shard_seed(5, info.rank)})
+        fn = _selftest_config(name) if a.selftest_cpu else CONFIGS[name]
+        r = fn(dev, st, a.steps, a.warmup, **kw)
         ms_rank = r["ms"]
         ms = shard.max_over_ranks(ms_rank, _DIST, dev)
         if name in SHARDED:
@@ -607,7 +638,8 @@ def main(argv=None):
                  wall_s=round(time.perf_counter() - t0, 1))
         if info.rank == 0:
             print(json.dumps(r), flush=True)
-        torch.cuda.empty_cache()
+        if not a.selftest_cpu:
+            torch.cuda.empty_cache()
     if _DIST is not None:
         _DIST.destroy_process_group()
     return 0
