@@ -780,3 +780,64 @@ def comb_minn_peak(M, smooth_win, gate_mask, search_bounds=None):
         raise ValueError("Minn peak detector received empty gate region")
     Ms = trailing_average(np.maximum(M, 0.0), max(1, smooth_win))
     return streaming_peak(Ms, mask)
+
+
+# ---------------------------------------------------------------------------------------
+# the back-end helpers one by one (core.py:123-138, 171-176, 339-370, 443-469) and
+# sync_aa.quantize_adc (sync_aa.py:263-291)
+# ---------------------------------------------------------------------------------------
+def apply_cfo(x, cfo, fs):
+    """core.py:123-138: x * exp(i 2 pi cfo n / fs), one tone for every branch of a 2-D x."""
+    x = np.asarray(x)
+    n = np.arange(x.shape[-1], dtype=float)
+    return x * np.exp(1j * 2 * np.pi * cfo * n / fs)
+
+
+def fft_used(sym, N, bins):
+    """core.py:171-176: fftshift(fft(sym, n=N))[(N/2 + k) % N]."""
+    spec = np.fft.fftshift(np.fft.fft(sym, n=N))
+    return spec[(N // 2 + np.asarray(bins)) % N]
+
+
+def cdiv_eps(y, d, eps):
+    """core.py:339-341 / :344-345: y / (d + eps)."""
+    return np.asarray(y) / (np.asarray(d) + eps)
+
+
+def remove_common_phase(x, ref=None):
+    """core.py:348-354."""
+    cpe = np.angle(np.mean(x)) if ref is None else np.angle(np.vdot(ref, x) / (np.vdot(ref, ref) + 1e-12))
+    return x * np.exp(-1j * cpe), float(cpe)
+
+
+def align_complex_gain(x, ref, eps=1e-12):
+    """core.py:357-362."""
+    g = np.vdot(x, ref) / (np.vdot(x, x) + eps)
+    return x * g, g
+
+
+def evm_rms_db(x, ref):
+    """core.py:365-370."""
+    e = float(np.sqrt(np.mean(np.abs(x - ref) ** 2) / np.mean(np.abs(ref) ** 2)))
+    return e, float(20 * np.log10(e + 1e-12))
+
+
+def phase_slope(h, bins, N):
+    """core.py:443-469 with abscissa = the centred subcarrier indices `bins`."""
+    if h.size == 0:
+        return 0.0, 0.0
+    k = np.asarray(bins, dtype=np.float64)
+    phi = np.unwrap(np.angle(h.astype(np.complex128)))
+    kz, pz = k - float(np.mean(k)), phi - float(np.mean(phi))
+    slope = float(np.sum(kz * pz) / (float(np.sum(kz * kz)) + 1e-12))
+    return slope, float(-slope * N / (2.0 * np.pi))
+
+
+def quantize_adc(samples, full_scale, bits=12):
+    """sync_aa.py:263-291 (numpy's own promotion decides float32 vs float64)."""
+    levels = 2 ** (bits - 1)
+
+    def q(v):
+        v = np.clip(v / full_scale, -1.0, 1.0 - 1.0 / levels)
+        return np.round(v * levels) / levels * full_scale
+    return q(samples.real) + 1j * q(samples.imag)

@@ -80,6 +80,32 @@ def test_oracle_matches_reference_golden(path):
         for k in ("evm", "evm_db", "slope", "sto"):
             assert abs(r[k] - float(d[k])) < 1e-9, k
         assert abs(r["gain"] - complex(d["gain"])) < 1e-12
+    elif kind == "backend_ops":
+        k = np.concatenate((np.arange(-600, 0), np.arange(1, 601)))
+        np.testing.assert_array_equal(O.apply_cfo(d["rx"], float(d["cfo"]), float(d["fs"])), d["rx_cfo"])
+        np.testing.assert_array_equal(O.fft_used(d["sym_p"], 2048, k), d["y_p"])
+        np.testing.assert_array_equal(O.fft_used(d["sym_p"][:2048 - 300], 2048, k), d["y_short"])
+        np.testing.assert_array_equal(O.cdiv_eps(d["y_p"], d["pil_used"], 1e-9), d["h"])
+        np.testing.assert_array_equal(O.cdiv_eps(d["y_d"], d["h"], 1e-9), d["xhat"])
+        x, c = O.remove_common_phase(d["xhat"])
+        np.testing.assert_array_equal(x, d["x_cpe"])
+        assert c == float(d["cpe"])
+        x, c = O.remove_common_phase(d["xhat"], d["dat_used"])
+        np.testing.assert_array_equal(x, d["x_cpe_ref"])
+        assert c == float(d["cpe_ref"])
+        xa, g = O.align_complex_gain(d["xhat"], d["dat_used"])
+        np.testing.assert_array_equal(xa, d["xa"])
+        assert g == complex(d["gain"])
+        assert O.evm_rms_db(d["xa"], d["dat_used"]) == (float(d["evm"]), float(d["evm_db"]))
+        assert O.phase_slope(d["h"], k, 2048) == (float(d["slope"]), float(d["sto"]))
+        x = np.atleast_2d(d["rx_cfo"])[0]
+        rms = float(d["rms"])
+        np.testing.assert_array_equal(O.quantize_adc(x, 4.0 * rms), d["q64"])
+        np.testing.assert_array_equal(O.quantize_adc(x, np.float64(2.5 * rms), 8), d["q64_np"])
+        q32 = O.quantize_adc(d["x32"], 3.0 * rms)
+        assert q32.dtype == np.complex64
+        np.testing.assert_array_equal(q32, d["q32"])
+        np.testing.assert_array_equal(O.quantize_adc(d["x32"], np.float64(3.0 * rms)), d["q32_np"])
     elif kind == "cp_search":
         x, N, cp, fs = d["x"], int(d["n_fft"]), int(d["cp_len"]), float(d["fs"])
         est = [int(e) for e in d["est"]]
