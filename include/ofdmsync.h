@@ -316,18 +316,22 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
  * For off in [0, T-(N+cp)]: 62-bin DFT of x[off+cp : off+cp+N] at fftshift positions
  * (N/2 + bin_indices) % N, metric = |sum_br vdot(t, bins)|^2 / max(E_t * sum_br sum|bins|^2, 1e-12).
  * bin_indices [n_bins] int32 and template_bins [n_bins] c128 are HOST pointers (n_bins <= 64);
- * metric: [B][T-(N+cp)+1] (device), f64 for OFS_FP64 (sliding DFT, n_br <= 4), f32 for
- * OFS_FP32 (per-window 64 x N/64 pruned FFT; needs OFS_C64, N = 64*2^j <= 4096 and at most
- * 64 offsets per stream: the cfg5 one-window-per-sequence shape).  Returns OFS_ESHORT when
- * T < N + cp (the reference raises ValueError).
+ * metric: [B][T-(N+cp)+1] (device), f64 for OFS_FP64, f32 for OFS_FP32.
+ *   OFS_FP64: sliding DFT in fp64 (zc_slide.hip: block-DFT-initialised chunks, four chunks per
+ *     wave; N a multiple of 64, n_br <= 2), else the one-chunk-per-wave sliding DFT (n_br <= 4).
+ *   OFS_FP32: few offsets per stream (<= 64, OFS_C64, N = 64*2^j <= 4096, the cfg5 shape): a
+ *     per-window 64 x N/64 pruned FFT in fp32; otherwise the fp64 sliding DFT of zc_slide.hip with
+ *     the metric rounded to fp32 (n_br <= 2, N a multiple of 64; else OFS_EINVAL).
+ * Returns OFS_ESHORT when T < N + cp (the reference raises ValueError).
  */
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                            int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
                            const int32_t* bin_indices, const double* template_bins,
                            double template_energy, void* metric, void* stream);
-/* which zc_freq kernel a shape runs on: 1 sliding DFT (fp64), 2 window FFT (fp32), 3 N = 4096
- * window FFT with the column sums reduced across lanes (fp32; taken when the template bins'
- * residues mod 64 are distinct, as the PSS template's are, otherwise 2), 0 none */
+/* which zc_freq kernel a one-branch shape runs on: 1 one-chunk-per-wave sliding DFT (fp64), 2 window
+ * FFT (fp32), 3 N = 4096 window FFT with the column sums reduced across lanes (fp32; taken when the
+ * template bins' residues mod 64 are distinct, as the PSS template's are, otherwise 2), 4 block-
+ * initialised sliding DFT (fp64), 5 the same with the metric rounded to fp32, 0 none */
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp);
 
 /*

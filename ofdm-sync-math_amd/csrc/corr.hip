@@ -1088,6 +1088,16 @@ int32_t ofs_zc_correlate(int32_t in_fmt, const void* x, int64_t B, int32_t n_br,
     }
 }
 
+// zc_slide.hip: the block-initialised sliding DFT (fp64 state; fp32 or fp64 metric out)
+extern "C" int ofs_zc_slide_ok(int fmt, int n_br, int N, int nbins, int64_t noff);
+extern "C" int ofs_zc_slide_launch(int fmt, int n_br, int out_f32, const void* x, int64_t B, int64_t T, int N, int cp,
+                                   int nbins, const int* kb, const double* tr, const double* ti, double t_energy,
+                                   void* metric, hipStream_t st);
+static bool zs_enabled() {                 // OFS_ZS=0: the earlier one-chunk-per-wave kernel (A/B)
+    const char* s = getenv("OFS_ZS");
+    return !(s && s[0] == '0');
+}
+
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                            int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
                            const int32_t* bin_indices, const double* template_bins,
@@ -1112,10 +1122,20 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
     }
     hipStream_t st = (hipStream_t)stream;
     if (precision == OFS_FP32) {
-        if (!zw_ok(in_fmt, precision, N, noff)) return OFS_EINVAL;
-        Zw64Args z;
-        if (N == 4096 && zw64_args(a, z) && zw64_enabled()) return zw64_launch(z, n_br, st);
-        return zw_launch(a, n_br, st);
+        if (zw_ok(in_fmt, precision, N, noff)) {          // few offsets per stream: window FFTs
+            Zw64Args z;
+            if (N == 4096 && zw64_args(a, z) && zw64_enabled()) return zw64_launch(z, n_br, st);
+            return zw_launch(a, n_br, st);
+        }
+        // many offsets: the fp64 sliding DFT, metric rounded to fp32 (its only fp32 step)
+        const int r = ofs_zc_slide_launch(in_fmt, n_br, 1, x, B, T, N, cp, n_bins, a.kb, a.tr, a.ti,
+                                          template_energy, metric, st);
+        return r == 1 ? OFS_OK : (r == 0 ? OFS_EINVAL : r);
+    }
+    if (zs_enabled()) {
+        const int r = ofs_zc_slide_launch(in_fmt, n_br, 0, x, B, T, N, cp, n_bins, a.kb, a.tr, a.ti,
+                                          template_energy, metric, st);
+        if (r != 0) return r == 1 ? OFS_OK : r;
     }
     if (n_br > 4) return OFS_EINVAL;
     // chunks of offsets: halve from ~N while the grid has fewer than OFS_ZF_ITEMS chunks in all
@@ -1135,10 +1155,10 @@ int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N
     const int64_t noff = T - ((int64_t)N + cp) + 1;
     if (noff <= 0) return 0;
     if (precision == OFS_FP32) {
-        if (!zw_ok(in_fmt, precision, N, noff)) return 0;
-        return (N == 4096 && zw64_enabled()) ? 3 : 2;
+        if (zw_ok(in_fmt, precision, N, noff)) return (N == 4096 && zw64_enabled()) ? 3 : 2;
+        return ofs_zc_slide_ok(in_fmt, 1, N, 62, noff) ? 5 : 0;
     }
-    return 1;
+    return (zs_enabled() && ofs_zc_slide_ok(in_fmt, 1, N, 62, noff)) ? 4 : 1;
 }
 
 int32_t ofs_zc_detect(const double* corr_mag, int64_t B, int64_t n, int32_t window_size,

@@ -1,8 +1,9 @@
 """Drop-in for the LTE-style frequency-domain ZC metric of ``zc_freq.py``.
 
 compute_frequency_metric (reference: zc_freq.py:62-99) runs on ``ofs_zc_freq_metric``
-(csrc/corr.hip): the 62 template bins of every window's N-point DFT are produced by a
-sliding DFT (one lane per bin, fp64), not by one FFT per offset.  ``N_FFT`` and
+(csrc/zc_slide.hip, csrc/corr.hip): the 62 template bins of every window's N-point DFT are
+produced by a sliding DFT in fp64 (not one FFT per offset); complex64 input returns float32
+(window FFTs in fp32 for a few offsets per stream, else the fp64 sliding DFT rounded to fp32).  ``N_FFT`` and
 ``CYCLIC_PREFIX`` are read from this module's globals at call time, like the reference.
 The template helpers are host-side setup of 62 constants (zc_freq.py:37-59).
 """
@@ -50,12 +51,11 @@ def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, templat
     if noff <= 0:
         raise ValueError("Received stream is shorter than a single OFDM symbol.")
     L = _lib.lib()
-    prec = _lib.resolve_precision(batch, precision)
-    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) not in (2, 3):
-        if precision is not None:
-            raise ValueError("fp32 zc_freq needs complex64 input, N = 64*2^j <= 4096 and <= 64 "
-                             "offsets per stream (the window-FFT kernel); use precision='fp64'")
-        prec = _lib.FP64                          # auto: the fp64 sliding-DFT kernel
+    prec = _lib.resolve_precision(batch, precision)     # complex64 -> fp32 result, whatever the offsets
+    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) not in (2, 3) and (
+            batch.nb > 2 or N % 64):
+        raise ValueError("fp32 zc_freq over many offsets needs N a multiple of 64 and <= 2 receive branches "
+                         "(the sliding-DFT kernel); use precision='fp64'")
     if prec == _lib.FP64 and batch.nb > 4:
         raise ValueError("the fp64 zc_freq kernel supports up to 4 receive branches")
     out = torch.empty((batch.B, noff), dtype=torch.float64 if prec == _lib.FP64 else torch.float32,
@@ -78,8 +78,9 @@ def compute_frequency_metric(rx_samples, bin_indices, template_bins, template_en
 
 def compute_frequency_metric_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                      N: int | None = None, cp: int | None = None, *, precision=None):
-    """Batched metric over x[B, n_branch, T] -> device tensor [B, T-(N+cp)+1]: f64 (sliding
-    DFT) or, for complex64 input with few offsets per stream, f32 (window FFT)."""
+    """Batched metric over x[B, n_branch, T] -> device tensor [B, T-(N+cp)+1]: f64 for complex128
+    / int16 input (sliding DFT), f32 for complex64 input (window FFT for <= 64 offsets per stream,
+    else the fp64 sliding DFT with the metric rounded to f32); ``precision`` overrides."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)

@@ -320,13 +320,65 @@ def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, monkeypatch):
     assert m.max() > 0.5
 
 
-def test_zc_freq_fp32_unsupported_shape_raises():
-    x = torch.zeros((1, 1, 5000), dtype=torch.complex64, device="cuda")
+def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
+    """complex64 input always returns float32: > 64 offsets per stream run the fp64 sliding DFT
+    with the metric rounded to fp32 (plan 5), within u·m of the fp64 kernel's result; shapes the
+    sliding kernel does not take (3 branches over many offsets) raise instead of switching."""
+    from ofdm_sync_amd import _lib
+    rng = np.random.default_rng(71)
+    x = rng_c(rng, 3, 2, 5000).astype(np.complex64)
+    x[1, :, 900:900 + 2048] += 3 * O.pss_symbol(2048)
     idx, t, e = O.zc_template()
-    with pytest.raises(ValueError):                # > 64 offsets per stream: no fp32 kernel
-        zc_freq.compute_frequency_metric_batched(x, idx, t, e, N=2048, cp=0, precision="fp32")
-    m = zc_freq.compute_frequency_metric_batched(x, idx, t, e, N=2048, cp=0)   # auto -> fp64
-    assert m.dtype == torch.float64
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, 5000, 2048, 0) == 5
+    xd = torch.from_numpy(x).cuda()
+    m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=2048, cp=0)     # auto -> fp32
+    assert m.dtype == torch.float32
+    m64 = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=2048, cp=0, precision="fp64")
+    assert m64.dtype == torch.float64
+    mm, m6 = m.cpu().numpy().astype(np.float64), m64.cpu().numpy()
+    assert np.all(np.abs(mm - m6) <= 2.0 ** -24 * m6 + 1e-30)          # one rounding to fp32
+    st = oracle_c.zc_freq_check(x, 2048, 0, idx, t, e, m.cpu().numpy(), 1e-12, 1.5)
+    print(f"fp32 many offsets: max |dm| {st[:, 0].max():.3g}, max |dm|/bound {st[:, 1].max():.3g}")
+    assert st[:, 1].max() <= 1.0 and mm[1].max() > 0.5
+    with pytest.raises(ValueError):                # 3 branches x many offsets: no fp32 kernel
+        zc_freq.compute_frequency_metric_batched(torch.zeros((1, 3, 5000), dtype=torch.complex64, device="cuda"),
+                                                 idx, t, e, N=2048, cp=0, precision="fp32")
+
+
+@pytest.mark.parametrize("fmt,N,cp,T,nb", [("c128", 2048, 512, 16384, 1), ("c128", 2048, 512, 4242, 2),
+                                           ("c64", 256, 64, 3001, 1), ("i16", 512, 0, 2600, 2),
+                                           ("c128", 64, 16, 700, 1), ("c128", 4096, 1024, 9000, 1),
+                                           ("c128", 8192, 0, 8300, 1), ("c128", 192, 5, 1000, 2),
+                                           ("c128", 2048, 512, 2600, 1)])
+def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
+    """The block-initialised sliding DFT (zc_slide.hip, plan 4) against the C oracle's fp64 FFTs on
+    every window (1e-9 relative + 1e-11) and against the earlier one-chunk-per-wave kernel (OFS_ZS=0):
+    odd T, cp offsets, chunks past the end, N not a power of two (192), N = 8192 (256-sample
+    blocks), offsets fewer than one chunk (T = 2600), int16 and complex64 input, two branches."""
+    from ofdm_sync_amd import _lib
+    rng = np.random.default_rng(N + T + nb)
+    B = 3
+    x = rng_c(rng, B, nb, T)
+    if T >= 400 + N:
+        x[0, :, 300:300 + N] += 3 * O.pss_symbol(N)
+    if fmt == "i16":
+        xi = np.stack([np.round(x.real * 300), np.round(x.imag * 300)], -1).astype(np.int16)
+        xd = torch.from_numpy(xi).cuda()
+        x = xi[..., 0] + 1j * xi[..., 1]
+    else:
+        x = x.astype(np.complex64 if fmt == "c64" else np.complex128)
+        xd = torch.from_numpy(x).cuda()
+    idx, t, e = O.zc_template()
+    assert _lib.lib().ofs_zc_freq_plan({"c128": _lib.C128, "c64": _lib.C64, "i16": _lib.CI16}[fmt], _lib.FP64, T, N,
+                                       cp) == 4
+    m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.setenv("OFS_ZS", "0")
+    m_prev = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.delenv("OFS_ZS")
+    np.testing.assert_allclose(m, m_prev, rtol=1e-9, atol=1e-11)
+    for b in range(B):
+        mo = O.zc_freq_metric(np.asarray(x[b], np.complex128), N, cp, idx, t, e)
+        np.testing.assert_allclose(m[b], mo, rtol=1e-9, atol=1e-11)
 
 
 @pytest.mark.parametrize("fmt,nb,N,T", [("c128", 1, 2048, 16384), ("c128", 2, 2048, 7000), ("c64", 3, 1024, 3000),

@@ -502,10 +502,31 @@ def zc_freq_fp64(dev, st, steps, warmup):
     x = torch.randn((B, 1, T), dtype=torch.complex128, device=dev, generator=g)
     ms = timed(lambda: zc_freq.compute_frequency_metric_batched(x, N=N, cp=cp), steps, warmup, st)
     noff = T - (N + cp) + 1
+    plan = _lib.lib().ofs_zc_freq_plan(_lib.C128, _lib.FP64, T, N, cp)
+    kern = {4: "zc_slide_kernel (block-initialised chunks, 4 chunks x 4 bins per lane)",
+            1: "zc_freq_kernel (lane = bin, one chunk per wave)"}.get(plan, str(plan))
     return _flops(dict(config="zc_freq_fp64", workload=f"zc_freq N={N} cp={cp}, {B} x {T} c128, fp64 sliding DFT",
-                       kernel="zc_freq_kernel<fp64> (lane = bin, sliding DFT)", samples=B * T, ms=ms,
+                       kernel=f"plan {plan}: {kern}", samples=B * T, ms=ms,
                        alg_bytes=B * T * 16 + B * noff * 8, bytes_per_sample="16 in + 8 out per offset"),
                   B * noff * 62 * 22, "fp64")
+
+
+def zc_freq_refshape(dev, st, steps, warmup, B=4096):
+    """zc_freq.compute_frequency_metric on the reference's own stream shape (zc_freq.run_simulation:
+    ~4.2k samples x 2 RX branches, N = 2048, cp = 512, ~1.7k offsets, zc_freq.py:102-147), complex64
+    batch of B streams -> float32 metric (plan 5: the fp64 sliding DFT, rounded to fp32).  Flops as
+    zc_freq_fp64 per (offset, bin) and branch-summed X."""
+    T, N, cp, nb = 4242, 2048, 512, 2
+    g = torch.Generator(device=dev).manual_seed(8)
+    x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    ms = timed(lambda: zc_freq.compute_frequency_metric_batched(x, N=N, cp=cp), steps, warmup, st)
+    noff = T - (N + cp) + 1
+    plan = _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp)
+    return _flops(dict(config="zc_freq_refshape", workload=f"zc_freq N={N} cp={cp}, {B} x {nb} x {T} c64 -> f32",
+                       kernel=f"plan {plan}: zc_slide_kernel (fp64 sliding DFT, block-initialised chunks, f32 out)",
+                       samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4,
+                       bytes_per_sample="8 in + 4 out per offset"),
+                  B * noff * 62 * (12 * nb + 10), "fp64")
 
 
 def zc_detect(dev, st, steps, warmup, state=False, seq=False):
@@ -536,7 +557,7 @@ def zc_detect(dev, st, steps, warmup, state=False, seq=False):
 
 
 CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "park_fp32": park, "park_fp64": lambda *a, **k: park(*a, prec="fp64", **k), "zc_mf": zc_mf,
-           "zc_freq_fp64": zc_freq_fp64, "zc_detect": zc_detect,
+           "zc_freq_fp64": zc_freq_fp64, "zc_freq_refshape": zc_freq_refshape, "zc_detect": zc_detect,
            "zc_detect_state": lambda *a, **k: zc_detect(*a, state=True, **k),
            "zc_detect_seq": lambda *a, **k: zc_detect(*a, seq=True, **k),
            "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
