@@ -6,21 +6,24 @@
 //     X_{s+1}[k] = w^{-k} (X_s[k] + x[s' + N] - x[s'])                    (the sliding recursion)
 //     metric(s) = |Σ_br Σ_k conj(t_k) X_s,br[k]|² / max(E_t Σ_br Σ_k |X_s,br[k]|², 1e-12)
 //
-// Work split (one workgroup = W waves = 4W consecutive chunks of C offsets of one stream):
-//   phase 1  block DFTs  β_k(m) = Σ_{j<C} x[cp + mC + j] w^{kj}  of the workgroup's 4W + N/C - 1
+// Work split (one workgroup = W waves = BPL·W consecutive chunks of C offsets of one stream):
+//   phase 1  block DFTs  β_k(m) = Σ_{j<C} x[cp + mC + j] w^{kj}  of the workgroup's BPL·W + N/C - 1
 //            blocks, one block per wave at a time (lane = bin, Horner in w^{4k} over four
 //            interleaved chains, samples broadcast from LDS), kept in LDS;
-//   phase 2  each wave slides FOUR chunks at once: row r = lanes 16r..16r+15 owns chunk 4w + r,
-//            lane (r, j) owns bins j, j+16, j+32, j+48 (64 slots; slots >= n_bins are held at 0).
-//            A chunk's initial window is Σ_{q<N/C} w^{kqC} β_k(c + q) (no per-chunk N-sample sum),
-//            then C steps of the recursion; per step the numerator / energy terms are summed
-//            in-lane over the lane's 4 bins and across the row's 16 lanes by DPP (quad_perm,
-//            row_ror: every lane gets the row total), and lane (r, u mod 16) keeps step u's result
-//            for one coalesced store per 16 steps.
+//   phase 2  each wave slides BPL chunks at once (BPL = bins per lane, 8 by default): a row of
+//            LPC = 64/BPL lanes owns one chunk, lane (r, j) owns bins j, j+LPC, ... (64 slots; slots
+//            >= n_bins have w^{-k} = 0 and stay 0).  A chunk's initial window is
+//            Σ_{q<N/C} w^{kqC} β_k(c + q) (no per-chunk N-sample sum), then C steps of the
+//            recursion; per step the numerator / energy terms are summed in-lane over the lane's
+//            BPL bins and across the row's LPC lanes by DPP (quad_perm, then row_half_mirror for
+//            8 lanes or row_ror 4/8 for 16: every lane gets the row total), and lane (r, u mod LPC)
+//            keeps step u's result for coalesced stores once per 16 steps.  More bins per lane =
+//            fewer cross-lane steps per offset (BPL 4 -> 8: 21 -> ~15 VALU per offset).
 // Every chunk starts from its own exact window (block sums), so the recursion runs at most C
 // steps (error ~C·2^-53 relative).  fp64 state throughout; OUT = float rounds only the metric.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <stdint.h>
 #include "ofdmsync.h"
 #include "ofs_common.h"
@@ -66,29 +69,37 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// sum over the 16 lanes of a row, result in every lane of the row: quad xor 1, xor 2, then
-// rotate the row by 4 and 8 (DPP quad_perm / row_ror; every lane has a source)
-__device__ __forceinline__ double row_sum16(double v) {
-    v += ofs::dpp_d<0xB1>(v);      // quad_perm [1,0,3,2]
-    v += ofs::dpp_d<0x4E>(v);      // quad_perm [2,3,0,1]
-    v += ofs::dpp_d<0x124>(v);     // row_ror:4
-    v += ofs::dpp_d<0x128>(v);     // row_ror:8
+constexpr int ZS_MAXW = 16;
+
+// sum over the LPC lanes of a row (8 or 16), result in every lane of the row
+template <int LPC>
+__device__ __forceinline__ double row_sum(double v) {
+    v += ofs::dpp_d<0xB1>(v);          // quad_perm [1,0,3,2]
+    v += ofs::dpp_d<0x4E>(v);          // quad_perm [2,3,0,1]
+    if constexpr (LPC == 8) {
+        v += ofs::dpp_d<0x141>(v);     // row_half_mirror: lane i <-> 7 - i within 8 lanes
+    } else {
+        v += ofs::dpp_d<0x124>(v);     // row_ror:4
+        v += ofs::dpp_d<0x128>(v);     // row_ror:8
+    }
     return v;
 }
 
-constexpr int ZS_MAXW = 16;
+constexpr int ZS_G = 16;               // steps per group (one d staging, one store round)
 
-template <int FMT, int NB, class OUT>
+template <int FMT, int NB, int BPL, class OUT>
 __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
+    constexpr int LPC = 64 / BPL;                                      // lanes per chunk row
     extern __shared__ __attribute__((aligned(16))) double2 zsm[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int W = a.W, C = a.C, N = a.N, NQ = N / C;
+    const int STG = C > ZS_G * BPL ? C : ZS_G * BPL;                  // per-wave staging per branch
     const int64_t b = blockIdx.x / a.groups, g = blockIdx.x - b * a.groups;
-    const int64_t c0 = g * 4 * (int64_t)W;
-    const int64_t c1 = min(c0 + 4 * (int64_t)W, a.nchunks);
+    const int64_t c0 = g * BPL * (int64_t)W;
+    const int64_t c1 = min(c0 + BPL * (int64_t)W, a.nchunks);
     const int nblk = (int)(c1 - c0) + NQ - 1;
     double2* beta = zsm;                                               // [nblk][NB][64]
-    double2* stg = zsm + (size_t)(4 * W + NQ - 1) * NB * 64 + (size_t)w * NB * C;   // per wave [NB][C]
+    double2* stg = zsm + (size_t)(BPL * W + NQ - 1) * NB * 64 + (size_t)w * NB * STG;   // per wave [NB][STG]
 
     // ---- phase 1: block DFTs (lane = bin slot) ----
     {
@@ -101,14 +112,14 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
             for (int r = 0; r < NB; ++r)
                 for (int j = lane; j < C; j += 64) {
                     const int64_t i = s0 + j;
-                    stg[r * C + j] = i < a.T ? ldx<FMT>(a.x, (b * NB + r) * a.T + i) : make_double2(0.0, 0.0);
+                    stg[r * STG + j] = i < a.T ? ldx<FMT>(a.x, (b * NB + r) * a.T + i) : make_double2(0.0, 0.0);
                 }
             wave_sync();
 #pragma unroll
             for (int r = 0; r < NB; ++r) {
                 double2 acc[4] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0),
                                   make_double2(0.0, 0.0)};
-                const double2* xs = stg + r * C;
+                const double2* xs = stg + r * STG;
                 for (int i = C / 4 - 1; i >= 0; --i) {
 #pragma unroll
                     for (int p = 0; p < 4; ++p) acc[p] = cfma(acc[p], z4, xs[4 * i + p]);
@@ -124,24 +135,22 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
     }
     __syncthreads();
 
-    // ---- phase 2: four chunks per wave, four bins per lane ----
-    const int row = lane >> 4, sl = lane & 15;
-    const int64_t c = c0 + 4 * (int64_t)w + row;                       // this row's chunk
-    if (c0 + 4 * (int64_t)w >= c1) return;                             // no chunk for the whole wave (no
+    // ---- phase 2: BPL chunks per wave, BPL bins per lane ----
+    const int row = lane / LPC, sl = lane % LPC;
+    const int64_t c = c0 + BPL * (int64_t)w + row;                     // this row's chunk
+    if (c0 + BPL * (int64_t)w >= c1) return;                           // no chunk for the whole wave (no
                                                                        // barrier follows)
     const bool live = c < c1;
     const int cl = live ? (int)(c - c0) : 0;                           // local block of the window start
-    double2 cq[4], tq[4], X[4][NB];
-    double dm[4];
+    double2 cq[BPL], tq[BPL], X[BPL][NB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int slot = sl + 16 * q;
+    for (int q = 0; q < BPL; ++q) {
+        const int slot = sl + LPC * q;
         const bool valid = slot < a.nbins;
         const int k = valid ? a.kb[slot] : 0;
         const double2 wk = twid(k, N);
-        cq[q] = make_double2(wk.x, -wk.y);                             // w^{-k}
+        cq[q] = valid ? make_double2(wk.x, -wk.y) : make_double2(0.0, 0.0);   // w^{-k}; 0 holds a slot at 0
         tq[q] = valid ? make_double2(a.tr[slot], a.ti[slot]) : make_double2(0.0, 0.0);
-        dm[q] = valid ? 1.0 : 0.0;
         const double2 step = twid(((int64_t)k * C) % N, N);            // w^{kC}
         double2 t = make_double2(1.0, 0.0);
 #pragma unroll
@@ -152,14 +161,17 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
             t = cmul(t, step);
         }
 #pragma unroll
-        for (int r = 0; r < NB; ++r) X[q][r] = make_double2(X[q][r].x * dm[q], X[q][r].y * dm[q]);
+        for (int r = 0; r < NB; ++r)
+            if (!valid) X[q][r] = make_double2(0.0, 0.0);
     }
-    double2* dbuf = stg;                                               // the wave's staging: [NB][4 rows][16]
+    double2* dbuf = stg;                                               // [NB][BPL rows][ZS_G]
     const int64_t o0 = c * (int64_t)C;
     OUT* out = static_cast<OUT*>(a.metric) + b * a.noff;
-    for (int og = 0; og < C; og += 16) {
-        {
-            const int64_t s = o0 + og + sl;                            // this lane's offset in the group
+    constexpr int KEEP = ZS_G / LPC;                                   // results kept per lane per group
+    for (int og = 0; og < C; og += ZS_G) {
+#pragma unroll
+        for (int j = 0; j < KEEP; ++j) {
+            const int64_t s = o0 + og + sl + LPC * j;                  // offsets of this lane's loads
             const int64_t i0 = a.cp + s;
 #pragma unroll
             for (int r = 0; r < NB; ++r) {
@@ -169,16 +181,18 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
                     const double2 u = ldx<FMT>(a.x, base + i0 + N), v = ldx<FMT>(a.x, base + i0);
                     d = make_double2(u.x - v.x, u.y - v.y);
                 }
-                dbuf[r * 64 + lane] = d;
+                dbuf[(r * BPL + row) * ZS_G + sl + LPC * j] = d;
             }
         }
         wave_sync();
-        double keep_n = 0.0, keep_e = 0.0;
+        double keep_n[KEEP], keep_e[KEEP];
+#pragma unroll
+        for (int j = 0; j < KEEP; ++j) { keep_n[j] = 0.0; keep_e[j] = 0.0; }
 #pragma unroll 2
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < ZS_G; ++u) {
             double cr = 0.0, ci = 0.0, e = 0.0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < BPL; ++q) {
                 double sr = X[q][0].x, si = X[q][0].y;
 #pragma unroll
                 for (int r = 1; r < NB; ++r) { sr += X[q][r].x; si += X[q][r].y; }
@@ -187,24 +201,29 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
 #pragma unroll
                 for (int r = 0; r < NB; ++r) e = fma(X[q][r].x, X[q][r].x, fma(X[q][r].y, X[q][r].y, e));
             }
-            cr = row_sum16(cr);
-            ci = row_sum16(ci);
-            e = row_sum16(e);
+            cr = row_sum<LPC>(cr);
+            ci = row_sum<LPC>(ci);
+            e = row_sum<LPC>(e);
             const double n2 = fma(cr, cr, ci * ci);
-            if (sl == u) { keep_n = n2; keep_e = e; }
+#pragma unroll
+            for (int j = 0; j < KEEP; ++j)
+                if (u == sl + LPC * j) { keep_n[j] = n2; keep_e[j] = e; }
 #pragma unroll
             for (int r = 0; r < NB; ++r) {
-                const double2 d = dbuf[r * 64 + row * 16 + u];
+                const double2 d = dbuf[(r * BPL + row) * ZS_G + u];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    X[q][r] = cmul(make_double2(fma(d.x, dm[q], X[q][r].x), fma(d.y, dm[q], X[q][r].y)), cq[q]);
+                for (int q = 0; q < BPL; ++q)
+                    X[q][r] = cmul(make_double2(X[q][r].x + d.x, X[q][r].y + d.y), cq[q]);
             }
         }
         wave_sync();                                                   // dbuf rewritten next group
-        const int64_t s = o0 + og + sl;
-        if (live && s < a.noff) {
-            const double den = a.t_energy * keep_e;
-            out[s] = (OUT)(keep_n / (den > 1e-12 ? den : 1e-12));
+#pragma unroll
+        for (int j = 0; j < KEEP; ++j) {
+            const int64_t s = o0 + og + sl + LPC * j;
+            if (live && s < a.noff) {
+                const double den = a.t_energy * keep_e[j];
+                out[s] = (OUT)(keep_n[j] / (den > 1e-12 ? den : 1e-12));
+            }
         }
     }
 }
@@ -213,13 +232,13 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
 
 namespace {
 template <int FMT, int NB, class OUT>
-int zs_go(ZsArgs& a, size_t lds, hipStream_t st) {
-    auto kern = zc_slide_kernel<FMT, NB, OUT>;
-    static bool attr = false;                        // the dynamic-LDS limit, once per instantiation
-    if (!attr) {
+int zs_go(ZsArgs& a, size_t lds, int bpl, hipStream_t st) {
+    auto kern = (NB == 2 || bpl == 4) ? zc_slide_kernel<FMT, NB, 4, OUT> : zc_slide_kernel<FMT, NB, NB == 2 ? 4 : 8, OUT>;
+    static bool attr[2] = {false, false};            // the dynamic-LDS limit, once per instantiation
+    if (!attr[bpl == 8]) {
         if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return OFS_EHIP;
-        attr = true;
+        attr[bpl == 8] = true;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)(a.B * a.groups)), dim3(64 * a.W), lds, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
@@ -229,12 +248,19 @@ int zs_go(ZsArgs& a, size_t lds, hipStream_t st) {
 namespace {
 // chunk / block length C (C | N; 256 for N >= 8192 keeps the blocks per window at <= 32), waves per
 // workgroup W (<= 16; 8 for two branches) and the workgroup's LDS; false if the blocks do not fit
-bool zs_plan(int n_br, int N, int64_t nchunks_of_C128, int& C, int& W, size_t& lds, int64_t noff) {
-    (void)nchunks_of_C128;
+// bins per lane of the slide: 8 for one branch (OFS_ZS_BPL=4 for the A/B), 4 for two (8 would
+// exceed the 128 VGPRs of a 16-wave workgroup and spill)
+int zs_bpl(int n_br) {
+    const char* s = getenv("OFS_ZS_BPL");
+    return (n_br == 2 || (s && atoi(s) == 4)) ? 4 : 8;
+}
+
+bool zs_plan(int n_br, int N, int bpl, int& C, int& W, size_t& lds, int64_t noff) {
     C = (N >= 8192 && N % 256 == 0) ? 256 : (N % 128 == 0 ? 128 : 64);
     const int64_t nchunks = (noff + C - 1) / C;
-    W = (int)std::min<int64_t>(n_br == 1 ? 16 : 8, (nchunks + 3) / 4);
-    auto lds_of = [&](int w) { return ((size_t)(4 * w + N / C - 1) * 64 + (size_t)w * C) * n_br * sizeof(double2); };
+    W = (int)std::min<int64_t>(n_br == 1 ? 16 : 8, (nchunks + bpl - 1) / bpl);
+    const int stg = C > 16 * bpl ? C : 16 * bpl;
+    auto lds_of = [&](int w) { return ((size_t)(bpl * w + N / C - 1) * 64 + (size_t)w * stg) * n_br * sizeof(double2); };
     while (W > 1 && lds_of(W) > 160 * 1024) --W;
     lds = lds_of(W);
     return lds <= 160 * 1024;
@@ -249,7 +275,7 @@ extern "C" int ofs_zc_slide_ok(int fmt, int n_br, int N, int nbins, int64_t noff
         return 0;
     int C, W;
     size_t lds;
-    return zs_plan(n_br, N, 0, C, W, lds, noff) ? 1 : 0;
+    return zs_plan(n_br, N, zs_bpl(n_br), C, W, lds, noff) ? 1 : 0;
 }
 
 // Launch (1), unsupported shape (0) or OFS_E*.  kb: template bins already reduced mod N (host).
@@ -268,13 +294,14 @@ extern "C" int ofs_zc_slide_launch(int fmt, int n_br, int out_f32, const void* x
         a.ti[i] = i < nbins ? ti[i] : 0.0;
     }
     size_t lds;
-    if (!zs_plan(n_br, N, 0, a.C, a.W, lds, noff)) return 0;
+    const int bpl = zs_bpl(n_br);
+    if (!zs_plan(n_br, N, bpl, a.C, a.W, lds, noff)) return 0;
     a.nchunks = (noff + a.C - 1) / a.C;
-    a.groups = (a.nchunks + 4 * a.W - 1) / (4 * a.W);
+    a.groups = (a.nchunks + (int64_t)bpl * a.W - 1) / ((int64_t)bpl * a.W);
     if (a.B * a.groups > 0x7fffffff) return 0;
     const bool f = out_f32 != 0;
 #define ZS_CASE(F, NBV) \
-    if (fmt == F && n_br == NBV) return f ? zs_go<F, NBV, float>(a, lds, st) : zs_go<F, NBV, double>(a, lds, st);
+    if (fmt == F && n_br == NBV) return f ? zs_go<F, NBV, float>(a, lds, bpl, st) : zs_go<F, NBV, double>(a, lds, bpl, st);
     ZS_CASE(OFS_C64, 1) ZS_CASE(OFS_C64, 2) ZS_CASE(OFS_C128, 1) ZS_CASE(OFS_C128, 2)
     ZS_CASE(OFS_CI16, 1) ZS_CASE(OFS_CI16, 2)
 #undef ZS_CASE
