@@ -86,6 +86,9 @@ __device__ __forceinline__ double row_sum(double v) {
 }
 
 constexpr int ZS_G = 16;               // steps per group (one d staging, one store round)
+#ifndef OFS_ZS_UNROLL
+#define OFS_ZS_UNROLL 2                // steps unrolled (tuning builds: -DOFS_ZS_UNROLL=1|4)
+#endif
 
 template <int FMT, int NB, int BPL, class OUT>
 __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
         double keep_n[KEEP], keep_e[KEEP];
 #pragma unroll
         for (int j = 0; j < KEEP; ++j) { keep_n[j] = 0.0; keep_e[j] = 0.0; }
-#pragma unroll 2
+#pragma unroll OFS_ZS_UNROLL
         for (int u = 0; u < ZS_G; ++u) {
             double cr = 0.0, ci = 0.0, e = 0.0;
 #pragma unroll

@@ -249,10 +249,17 @@ def backend(dev, st, steps, warmup):
             outs[1].data_ptr(), outs[2].data_ptr(), outs[3].data_ptr(), outs[4].data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_rx_backend(*args), "rx_backend"), steps, warmup, st)
     nbytes = B * (nb * (2 * N + 2 * cp) * 8 + 2 * U * 16 + 5 * 8 + 16)
-    return dict(config="backend", workload=f"receiver back-end, {B} frames x {nb} branches, N={N}, CP={cp}, c64 in, fp64",
-                kernel="rx_backend_kernel (LDS radix-2 FFTs, one workgroup per frame)", samples=B * nb * 2 * N,
-                ms=ms, alg_bytes=nbytes, bytes_per_sample="windows read once (8 B) + 2 x 16 B per used bin out",
-                frames_per_s=round(B / (ms / 1e3), 1))
+    # fp64 flops per frame (DESIGN.md §7 back-end roofline): CP correlation 8 per branch-sample;
+    # two windows: per branch a complex tone product + accumulate (8) and the tone rotation (6) per
+    # sample; two radix-2 FFTs 5 N log2 N; per used bin: two numpy divisions (11 each), unwrap +
+    # fit (~12), vdot / EVM sums and the gain product (~20)
+    lg = int(np.log2(N))
+    flops = 8 * cp * nb + 2 * (N * nb * 8 + N * 6) + 2 * 5 * N * lg + U * (11 + 11 + 12 + 20)
+    return _flops(dict(config="backend",
+                       workload=f"receiver back-end, {B} frames x {nb} branches, N={N}, CP={cp}, c64 in, fp64",
+                       kernel="rx_backend_kernel (LDS radix-2 FFTs, one workgroup per frame)", samples=B * nb * 2 * N,
+                       ms=ms, alg_bytes=nbytes, bytes_per_sample="windows read once (8 B) + 2 x 16 B per used bin out",
+                       frames_per_s=round(B / (ms / 1e3), 1), flops_per_frame=flops), B * flops, "fp64")
 
 
 def cfg3_2ant(dev, st, steps, warmup):
@@ -482,12 +489,29 @@ def zc_mf(dev, st, steps, warmup, method="fft"):
     ms = timed(lambda: zc_v2.correlate_batched(x, ref, zc_v2.OFS_ZC_V2, want_corr=True, want_mag=True,
                                                method=method), steps, warmup, st)
     nout = T + N - 1
+    # traffic model of the FFT path (bytes every pass moves): blocks of M samples
+    # (ofs_zc_mf_plan_create's pick_m: power of two >= 2N minimising nblk·M), rows = B·nblk spectra
+    M, best = 0, None
+    for m in (1 << e for e in range(1, 17)):
+        if m < 2 * N or m < 1024:
+            continue
+        nblk_m = -(-nout // (m - N + 1))
+        if best is None or nblk_m * m < best:
+            best, M = nblk_m * m, m
+    nblk = -(-nout // (M - N + 1))
+    spec = B * nblk * M * 16
+    traffic = (B * T * 16 + spec) + 2 * spec + 2 * spec + 2 * spec + (B * nout * 16 + B * T * 16 + B * nout * 24)
     r = dict(config="zc_mf" if method == "fft" else "zc_mf_direct",
              workload=f"zc_v2 matched filter + normalise, N={N} taps, {B} x {T} c128, fp64",
              kernel=("FFT overlap-save: pack + rocFFT fwd + xH + rocFFT inv + extract/normalise (fp64)"
                      if method == "fft" else "zc_mf_kernel<fp64> (direct correlation, LDS tile)"),
              samples=B * T, ms=ms, alg_bytes=B * T * 16 + B * nout * 24,
              bytes_per_sample="16 in + corr 16 + |corr| 8 out")
+    if method == "fft":
+        r.update(fft_block=M, fft_blocks=nblk, traffic_model_bytes=traffic,
+                 traffic_model="pack (x in, spectra out) + rocFFT fwd (r+w) + xH (r+w) + rocFFT inv (r+w) + extract "
+                               "(valid spectra + x for the energy prefix in, corr + |corr| out)",
+                 traffic_frac=round(traffic / (ms / 1e3) / 1e9 / HBM, 4))
     # the direct-sum work (8N flops per output) is the reference's algorithm; the FFT path does far
     # less arithmetic, so its flop_frac is quoted against the direct count ("direct-equivalent")
     return _flops(r, B * nout * (8 * N + 4), "fp64")
