@@ -438,6 +438,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     double CC = 0.0, CE = 0.0;
     double sm = 0.0;                                               // IIR state carried between segments
     long long si = 0;
+#if OFS_RTL_ROUNDS_DEBUG
+    long long dbg_rounds = 0;
+#endif
     AaRowGate<SC, double, true, true, false> gate;                 // detect_minn_rtl, closed form
     if (a.detect)
         gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
@@ -632,6 +635,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                         own[e] = st;
                     }
                     const double prev_leave = ofs::wave_shr1(st, lane, sm);
+#if OFS_RTL_ROUNDS_DEBUG
+                    ++dbg_rounds;
+#endif
                     if (__ballot(!same_bits(enter, prev_leave)) == 0) {
                         sm = readlane(st, 63);
                         break;
@@ -688,6 +694,10 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
         __builtin_amdgcn_wave_barrier();                               // LDS reuse by the next segment
     }
     if (a.detect) gate.finish(lane, (int)T, a.n_ev + b, a.open_start ? a.open_start + b : nullptr);
+#if OFS_RTL_ROUNDS_DEBUG                    // tools/rtl_rounds.py: speculation rounds over the stream
+    __builtin_amdgcn_wave_barrier();
+    if (a.open_start && lane == 0) a.open_start[b] = dbg_rounds;
+#endif
 }
 
 // ---- dispatch -------------------------------------------------------------------------------

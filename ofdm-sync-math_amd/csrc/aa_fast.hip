@@ -91,8 +91,9 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 #ifndef OFS_FAST_FF
 #define OFS_FAST_FF 0
 #endif
-// DO: detect-only instantiation (P/R/M/valid not stored, events only: SURVEY §8d)
-template <int E, int MR, int NA, bool DO>
+// DO: detect-only instantiation (P/R/M/valid not stored, events only: SURVEY §8d); S32: fp32
+// row scans (ofs_common.h row_scan; the detect-only default, issue-bound there)
+template <int E, int MR, int NA, bool DO, bool S32>
 __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     constexpr int RL = 64 * E;                 // samples per row
     constexpr int RW = TMAX / RL;              // rows per stream
@@ -213,7 +214,7 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 #pragma unroll
             for (int e = E - 2; e >= 0; --e) { gS[e] = gS[e + 1] + av[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
             // ---- lane totals: fp64 DPP wave scan, row totals, rows inside the window ----
-            const RowScan sRr = row_scan(fS[E - 1].x), sIr = row_scan(fS[E - 1].y), sEr = row_scan(fE[E - 1]);
+            const RowScan sRr = row_scan<S32>(fS[E - 1].x), sIr = row_scan<S32>(fS[E - 1].y), sEr = row_scan<S32>(fE[E - 1]);
             const double totR = sRr.tot, totI = sIr.tot, totE = sEr.tot;
             const pf2 xS = pf2{sRr.x, sIr.x};                        // lanes < l
             const float xE = sEr.x;
@@ -417,13 +418,13 @@ struct AaStream {
         gS[E - 1] = pf2{0.f, 0.f}; gE[E - 1] = 0.f;
 #pragma unroll
         for (int e = E - 2; e >= 0; --e) { gS[e] = gS[e + 1] + av[e + 1]; gE[e] = gE[e + 1] + aE[e + 1]; }
-        const RowScan se_ = row_scan(fE[E - 1]);
+        const RowScan se_ = row_scan<false>(fE[E - 1]);
         const double tE = se_.tot;
         const float xE = se_.x, uE = se_.u;
         double tR = 0.0, tI = 0.0;
         pf2 xS = pf2{0.f, 0.f}, uS = pf2{0.f, 0.f};
         if (!FIRST) {                                        // no lagged product before row MR
-            const RowScan sr_ = row_scan(fS[E - 1].x), si_ = row_scan(fS[E - 1].y);
+            const RowScan sr_ = row_scan<false>(fS[E - 1].x), si_ = row_scan<false>(fS[E - 1].y);
             tR = sr_.tot; tI = si_.tot;
             xS = pf2{sr_.x, si_.x};
             uS = pf2{sr_.u, si_.u};
@@ -558,14 +559,24 @@ int launch_stream_mr(int mr, const AaFastArgs& a, hipStream_t st) {
     return 0;
 }
 
+// row-scan precision of the register-staged kernel, read per call: the detect-only launch scans
+// in fp32 unless OFS_FAST_SCAN_DO=64, the storing launch in fp64 unless OFS_FAST_SCAN=32 (tests
+// run the storing kernel with the detect-only arithmetic to classify its events, A/B)
+bool scan32(bool det_only) {
+    const char* s = getenv(det_only ? "OFS_FAST_SCAN_DO" : "OFS_FAST_SCAN");
+    if (s && (s[0] == '3' || s[0] == '6')) return s[0] == '3';
+    return det_only;
+}
+
 template <int E, int MR, int NA>
 int launch(const AaFastArgs& a, hipStream_t st) {
     const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
-    const int64_t grid = (a.B + FAST_WG / 64 - 1) / (FAST_WG / 64);
-    if (det_only)
-        hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
-    else
-        hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(FAST_WG), 0, st, a);
+    const bool s32 = scan32(det_only);
+    const dim3 grid((unsigned)((a.B + FAST_WG / 64 - 1) / (FAST_WG / 64))), blk(FAST_WG);
+    if (det_only && s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, true>), grid, blk, 0, st, a);
+    else if (det_only) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, false>), grid, blk, 0, st, a);
+    else if (s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, false>), grid, blk, 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
@@ -600,12 +611,13 @@ int pick_e(int L) {
 }
 
 // detect-only (events without P/R/M stores: VALU/issue-bound, not HBM-bound, SQ counters r03a):
-// samples per lane per row.  Wider rows amortise the three fp64 DPP row scans (lane totals of
-// Re P, Im P, R: ~25 VALU each per row) over more samples; override with OFS_FAST_E_DO=2|4|8.
+// samples per lane per row.  With fp32 row scans (3 x ~7 VALU per row instead of ~25) E = 4 is
+// the fastest (r03f: 0.1071 ms vs 0.1134 at E = 8, 0.1191 / 0.1193 with fp64 scans at E = 4 / 8);
+// override with OFS_FAST_E_DO=2|4|8.
 int pick_e_do(int L) {
     const char* s = getenv("OFS_FAST_E_DO");
     const int forced = s ? atoi(s) : 0;
-    for (int e : {forced, 8, 4, 2})
+    for (int e : {forced, 4, 8, 2})
         if ((e == 2 || e == 4 || e == 8) && L % (64 * e) == 0) return e;
     return 0;
 }

@@ -189,23 +189,22 @@ __device__ __forceinline__ float scan_add_f32(float v) {
 }
 
 // Scan of one lane value across a row (the wave): x = sum over lanes < l, u = sum over lanes > l,
-// tot = the row total.  fp64 by default; OFS_SCAN32 (tuning builds) scans in fp32: the sums are
-// of one row's terms only (no cancellation against a stream-wide prefix), error ~6 ulp of the row.
-#ifndef OFS_SCAN32
-#define OFS_SCAN32 0
-#endif
+// tot = the row total.  F32 = false: fp64 ladder (x, u exact to fp32 rounding, tot exact);
+// F32 = true: fp32 ladder, 6 rounded adds deep: the sums are of one row's lane totals only (no
+// cancellation against a stream-wide prefix), so |dx|, |dtot| <= 6u·Σ_row|v| and |du| <= 13u·Σ_row|v|
+// (the detect-only kernel: half the issue slots of the fp64 ladder, r03f).
 struct RowScan { float x, u; double tot; };
+template <bool F32>
 __device__ __forceinline__ RowScan row_scan(float v) {
-#if OFS_SCAN32
-    const float i = scan_add_f32(v);
-    const float t = readlane(i, 63);
-    return RowScan{__int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(i), 0x138, 0xf, 0xf, true)), t - i,
-                   (double)t};
-#else
-    const double i = scan_add((double)v);
-    const double t = readlane(i, 63);
-    return RowScan{(float)shr1z(i), (float)(t - i), t};
-#endif
+    if constexpr (F32) {
+        const float i = scan_add_f32(v);
+        const float t = readlane(i, 63);
+        return RowScan{dppz_f<0x138>(i), t - i, (double)t};
+    } else {
+        const double i = scan_add((double)v);
+        const double t = readlane(i, 63);
+        return RowScan{(float)shr1z(i), (float)(t - i), t};
+    }
 }
 
 

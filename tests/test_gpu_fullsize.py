@@ -118,15 +118,18 @@ def test_cfg4_fused_shard_every_stream_vs_oracle():
 def test_cfg3_detect_only_full_batch_vs_oracle(monkeypatch):
     """The headline batch with P/R/M not stored (SURVEY §8d detect-only): every stream's events
     against the C oracle (oracle/parity.py: exact except stated near-ties; CFO angle <= 1e-6).
-    The detect-only kernel runs 8 samples per lane per row (aa_fast.hip pick_e_do); the M the
-    classifier needs comes from the storing kernel forced to the same row width, i.e. the same
-    arithmetic, so both calls' events are identical too."""
+    The detect-only kernel runs 4 samples per lane per row with fp32 row scans (aa_fast.hip
+    pick_e_do, scan32); the M the classifier needs comes from the storing kernel forced to the
+    same row width and scan precision, i.e. the same arithmetic, so both calls' events are
+    identical too."""
     import parity
     B, T, L = 65536, 1024, 512
     x = synth.headline_batch(B, T, L, seed=777)
-    monkeypatch.setenv("OFS_FAST_E", "8")
+    monkeypatch.setenv("OFS_FAST_E", "4")
+    monkeypatch.setenv("OFS_FAST_SCAN", "32")
     full = sync_aa.aa_detect_streaming_batched(x, L, outputs=("M",), max_events=8)
     monkeypatch.delenv("OFS_FAST_E")
+    monkeypatch.delenv("OFS_FAST_SCAN")
     det = sync_aa.aa_detect_streaming_batched(x, L, outputs=(), max_events=8)
     assert torch.equal(full.n_events, det.n_events)
     k = int(min(det.n_events.max(), 8))

@@ -377,8 +377,11 @@ def cfg3_detect(dev, st, steps, warmup):
             0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa detect-only"), steps, warmup, st)
     stored = int(torch.clamp(n_ev, max=E).sum().item())
+    ed = int(os.environ.get("OFS_FAST_E_DO", "4"))
+    scan = "fp64" if os.environ.get("OFS_FAST_SCAN_DO", "32").startswith("6") else "fp32"
     return dict(config="cfg3_detect", workload=f"sync_aa S&C fp32 detect-only, L={L}, {B} x {T} c64 (events only)",
-                kernel="aa_fast_kernel<E=2,MR=4> with P/R/M stores off", samples=B * T, ms=ms,
+                kernel=f"aa_fast_kernel<E={ed},MR={L // (64 * ed)},DO,{scan} row scans> (P/R/M stores off)",
+                samples=B * T, ms=ms,
                 alg_bytes=B * T * 8 + B * 4 + stored * 64,
                 bytes_per_sample="8 in + 4 B/stream + 64 B/event", events_per_stream=round(stored / B, 3))
 
