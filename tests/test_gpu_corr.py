@@ -351,8 +351,9 @@ def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
                                            ("c128", 8192, 0, 8300, 1), ("c128", 192, 5, 1000, 2),
                                            ("c128", 2048, 512, 2600, 1)])
 def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
-    """The block-initialised sliding DFT (zc_slide.hip, plan 4) against the C oracle's fp64 FFTs on
-    every window (1e-9 relative + 1e-11) and against the earlier one-chunk-per-wave kernel (OFS_ZS=0):
+    """The block-initialised sliding DFT (zc_slide.hip, plan 4: the pair resonators for the ZC template's
+    ±k bins) against the C oracle's fp64 FFTs on every window (1e-9 relative + 1e-11), against the
+    per-bin recursion (OFS_ZS_PAIR=0) and the earlier one-chunk-per-wave kernel (OFS_ZS=0):
     odd T, cp offsets, chunks past the end, N not a power of two (192), N = 8192 (256-sample
     blocks), offsets fewer than one chunk (T = 2600), int16 and complex64 input, two branches."""
     from ofdm_sync_amd import _lib
@@ -376,9 +377,58 @@ def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
     m_prev = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
     monkeypatch.delenv("OFS_ZS")
     np.testing.assert_allclose(m, m_prev, rtol=1e-9, atol=1e-11)
+    monkeypatch.setenv("OFS_ZS_DEFER", "0")        # per-step DPP row sums instead of the LDS partials
+    m_dpp = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.delenv("OFS_ZS_DEFER")
+    np.testing.assert_allclose(m, m_dpp, rtol=1e-12, atol=1e-14)
+    monkeypatch.setenv("OFS_ZS_PAIR", "0")         # first-order recursion per bin instead of the pair resonators
+    m_bin = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.delenv("OFS_ZS_PAIR")
+    np.testing.assert_allclose(m, m_bin, rtol=1e-9, atol=1e-11)
     for b in range(B):
         mo = O.zc_freq_metric(np.asarray(x[b], np.complex128), N, cp, idx, t, e)
         np.testing.assert_allclose(m[b], mo, rtol=1e-9, atol=1e-11)
+
+
+@pytest.mark.parametrize("tmpl,nb", [("zc_shuffled", 1), ("random_pairs", 1), ("random_pairs", 2),
+                                     ("unpaired", 1), ("with_dc", 2), ("one_pair", 1)])
+def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
+    """Template shapes around the pair kernel's condition (every bin k has its mirror N - k, neither
+    0 nor N/2): ZC bins in shuffled slot order, random complex template values on paired bins (the
+    A/B constants), an unpaired set and a set with the DC bin (both take the per-bin recursion), a
+    single pair.  Each against the C oracle's direct DFT (1e-9 relative + 1e-11) and the per-bin
+    kernel (OFS_ZS_PAIR=0)."""
+    from ofdm_sync_amd import _lib
+    N, cp, T = 2048, 512, 6000
+    rng = np.random.default_rng(hash(tmpl) % 1000 + nb)
+    idx, t, e = O.zc_template()
+    if tmpl == "zc_shuffled":
+        perm = rng.permutation(idx.size)
+        idx, t = idx[perm], t[perm]
+    elif tmpl == "random_pairs":
+        k = rng.choice(np.arange(1, 200), 20, replace=False)
+        idx = np.concatenate((k, -k))[rng.permutation(40)]
+        t = rng_c(rng, idx.size)
+    elif tmpl == "unpaired":
+        idx = np.arange(1, 40)
+        t = rng_c(rng, idx.size)
+    elif tmpl == "with_dc":
+        idx = np.arange(-20, 21)
+        t = rng_c(rng, idx.size)
+    elif tmpl == "one_pair":
+        idx, t = np.array([-7, 7]), np.array([1.0 + 0.5j, -0.25 + 1j])
+    e = float(np.sum(np.abs(t) ** 2))
+    x = rng_c(rng, 2, nb, T)
+    x[0, :, 700:700 + N] += 3 * O.pss_symbol(N)
+    xd = torch.from_numpy(x).cuda()
+    m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.setenv("OFS_ZS_PAIR", "0")
+    m_bin = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    monkeypatch.delenv("OFS_ZS_PAIR")
+    np.testing.assert_allclose(m, m_bin, rtol=1e-9, atol=1e-11)
+    for b in range(2):
+        np.testing.assert_allclose(m[b], O.zc_freq_metric(x[b], N, cp, idx, t, e), rtol=1e-9, atol=1e-11)
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C128, _lib.FP64, T, N, cp) == 4
 
 
 @pytest.mark.parametrize("fmt,nb,N,T", [("c128", 1, 2048, 16384), ("c128", 2, 2048, 7000), ("c64", 3, 1024, 3000),

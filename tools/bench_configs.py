@@ -522,15 +522,18 @@ def zc_mf(dev, st, steps, warmup, method="fft"):
 
 def zc_freq_fp64(dev, st, steps, warmup):
     """zc_freq.compute_frequency_metric (zc_freq.py:62-99) at the reference's N = 2048, cp = 512, fp64
-    sliding DFT: B = 256 x T = 16384 c128.  Per offset and template bin: window update (x[s+N] -
-    x[s])·w^{ks} (6 + 2 flops), twiddle advance (6), vdot term (8): ~22 flops x 62 bins."""
+    sliding DFT: B = 256 x T = 16384 c128.  Work unit (algorithm-independent, like the direct-sum
+    count of the FFT matched filter): the first-order sliding DFT per offset and template bin -
+    window update (x[s+N] - x[s])·w^{ks} (6 + 2 flops), twiddle advance (6), vdot term (8): ~22 flops
+    x 62 bins.  The pair kernel (±k resonators, Goertzel block DFTs) issues fewer instructions than
+    this model counts; its VALU issue share is in the SQ counters (profiles/)."""
     B, T, N, cp = 256, 16384, 2048, 512
     g = torch.Generator(device=dev).manual_seed(6)
     x = torch.randn((B, 1, T), dtype=torch.complex128, device=dev, generator=g)
     ms = timed(lambda: zc_freq.compute_frequency_metric_batched(x, N=N, cp=cp), steps, warmup, st)
     noff = T - (N + cp) + 1
     plan = _lib.lib().ofs_zc_freq_plan(_lib.C128, _lib.FP64, T, N, cp)
-    kern = {4: "zc_slide_kernel (block-initialised chunks, 4 chunks x 4 bins per lane)",
+    kern = {4: "zc_pair_kernel (±k Goertzel resonators, 8 chunks x 4 pairs per lane, Goertzel block DFTs)",
             1: "zc_freq_kernel (lane = bin, one chunk per wave)"}.get(plan, str(plan))
     return _flops(dict(config="zc_freq_fp64", workload=f"zc_freq N={N} cp={cp}, {B} x {T} c128, fp64 sliding DFT",
                        kernel=f"plan {plan}: {kern}", samples=B * T, ms=ms,
@@ -550,7 +553,7 @@ def zc_freq_refshape(dev, st, steps, warmup, B=4096):
     noff = T - (N + cp) + 1
     plan = _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp)
     return _flops(dict(config="zc_freq_refshape", workload=f"zc_freq N={N} cp={cp}, {B} x {nb} x {T} c64 -> f32",
-                       kernel=f"plan {plan}: zc_slide_kernel (fp64 sliding DFT, block-initialised chunks, f32 out)",
+                       kernel=f"plan {plan}: zc_pair_kernel (fp64 ±k Goertzel resonators, 4 chunks x 2 pairs per lane, f32 out)",
                        samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4,
                        bytes_per_sample="8 in + 4 out per offset"),
                   B * noff * 62 * (12 * nb + 10), "fp64")
