@@ -154,7 +154,8 @@ def cfg2b(dev, st, steps, warmup, cp12=False, B=4096):
         ptrs = [ptrs[0], ptrs[1], None, ptrs[3], None, ptrs[5], ptrs[6], None]
     det = 0 if parts in ("metric", "smooth") else 1
     fmt = _lib.CP12 if cp12 else _lib.CI16
-    args = (fmt, x.data_ptr(), B, 1, T, Q, 3, 0, 3276, 15, *ptrs, det, 2, 0, E,
+    smode = int(os.environ.get("OFS_CFG2B_MODE", "0"))     # 1: the RTL floor-shift smoothing
+    args = (fmt, x.data_ptr(), B, 1, T, Q, 3, smode, 3276, 15, *ptrs, det, 2, 0, E,
             n_ev.data_ptr(), ev.data_ptr(), og.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_minn_rtl(*args), "minn_rtl"), steps, warmup, st)
     insz = 3 if cp12 else 4
