@@ -20,6 +20,7 @@
 // Per-frame, O(N log N) work: compute-bound and tiny next to the metric kernels.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include <math.h>
 #include <stdint.h>
 #include "ofdmsync.h"
@@ -156,9 +157,11 @@ __device__ double unwrap_slope(double* ph, const int32_t* bins, int U, double* r
         double local = 0.0;
         for (int u = max(u0, 1); u < u1; ++u) {
             const double dd = ph[u] - ph[u - 1];
-            double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
-            if (dm == -M_PI && dd > 0.0) dm = M_PI;
-            local += fabs(dd) < M_PI ? 0.0 : dm - dd;
+            if (!(fabs(dd) < M_PI)) {                        // numpy's correction only where |dd| >= pi
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                local += dm - dd;
+            }
         }
         // exclusive block scan of the per-thread totals
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -180,9 +183,11 @@ __device__ double unwrap_slope(double* ph, const int32_t* bins, int U, double* r
             const double raw = ph[u];
             if (u >= 1) {
                 const double dd = raw - prev_raw;
-                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
-                if (dm == -M_PI && dd > 0.0) dm = M_PI;
-                run += fabs(dd) < M_PI ? 0.0 : dm - dd;
+                if (!(fabs(dd) < M_PI)) {
+                    double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                    if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                    run += dm - dd;
+                }
             }
             prev_raw = raw;
             ph[u] = raw + run;
@@ -229,6 +234,384 @@ __device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, d
         tone = cmul(tone, step);
     }
     lds_barrier();
+}
+
+template <int FMT> struct BeRaw { using T = float2; };          // the input word kept in registers
+template <> struct BeRaw<OFS_C128> { using T = double2; };
+template <> struct BeRaw<OFS_CI16> { using T = short2; };
+template <int FMT>
+__device__ __forceinline__ typename BeRaw<FMT>::T ld_raw(const void* p, int64_t i) {
+    return static_cast<const typename BeRaw<FMT>::T*>(p)[i];
+}
+template <class T>
+__device__ __forceinline__ double2 widen(T v) { return make_double2((double)v.x, (double)v.y); }
+template <class T>
+__device__ __forceinline__ T zero_raw() { T z; z.x = 0; z.y = 0; return z; }
+
+constexpr int BE_CPT = 2;                     // CP samples per thread (cp <= 2·BW on the fast path)
+
+// one window of NBT branches, SPT samples per thread, raw words.  A window wholly inside [0, T)
+// (the usual case, one wave-uniform test) loads without per-element guards, from one base pointer
+// per branch, so the loads need no per-element 64-bit address or condition registers.
+template <int FMT, int SPT, int NBT>
+struct BeWindow {
+    typename BeRaw<FMT>::T v[NBT][SPT];
+    __device__ __forceinline__ void issue(const BeArgs& a, int64_t b, int64_t s) {
+        using T = typename BeRaw<FMT>::T;
+        const T* x = static_cast<const T*>(a.x);
+        if (s >= 0 && s + SPT * BW <= a.T) {
+#pragma unroll
+            for (int r = 0; r < NBT; ++r) {
+                const T* p = x + (b * NBT + r) * a.T + s + threadIdx.x;
+#pragma unroll
+                for (int m = 0; m < SPT; ++m) v[r][m] = p[BW * m];
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < NBT; ++r)
+#pragma unroll
+                for (int m = 0; m < SPT; ++m) {
+                    const int64_t i = s + threadIdx.x + BW * m;
+                    v[r][m] = (i >= 0 && i < a.T) ? x[(b * NBT + r) * a.T + i] : zero_raw<T>();
+                }
+        }
+    }
+};
+// the CP correlation's samples x[ps + n], x[ps + N + n], n = tid + BW·m < cp
+template <int FMT, int NBT>
+struct BeCp {
+    typename BeRaw<FMT>::T u[NBT][BE_CPT], w[NBT][BE_CPT];
+    __device__ __forceinline__ void issue(const BeArgs& a, int64_t b, int64_t ps) {
+        using T = typename BeRaw<FMT>::T;
+        const T* x = static_cast<const T*>(a.x);
+        const bool full = ps >= 0 && ps + a.N + a.cp <= a.T;
+#pragma unroll
+        for (int r = 0; r < NBT; ++r) {
+            const T* p = x + (b * NBT + r) * a.T + ps + threadIdx.x;
+#pragma unroll
+            for (int m = 0; m < BE_CPT; ++m) {
+                const int n = threadIdx.x + BW * m;
+                const int64_t i0 = ps + n, i1 = ps + a.N + n;
+                const bool ok = !a.cfo_in && n < a.cp && (full || (i0 >= 0 && i1 < a.T));
+                u[r][m] = ok ? p[BW * m] : zero_raw<T>();
+                w[r][m] = ok ? p[a.N + BW * m] : zero_raw<T>();
+            }
+        }
+    }
+};
+
+// window (registers) -> rx_eff = mean_br(x · exp(-i 2 pi cfo n / fs)) bit-reversed into buf
+template <int FMT, int SPT, int NBT>
+__device__ __forceinline__ void place_window(const BeArgs& a, int64_t s, double cfo, const BeWindow<FMT, SPT, NBT>& win,
+                                             double2* buf, int LB) {
+    const double w0 = 2.0 * M_PI * (-cfo);
+    double sn, cs, ss, cc;
+    sincos(w0 * (double)(s + (int64_t)threadIdx.x) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    sincos(w0 * (double)BW / a.fs, &ss, &cc);
+    double2 tone = make_double2(cs, sn);
+    const double2 step = make_double2(cc, ss);
+    const int rb = bitrev(threadIdx.x, LB);
+#pragma unroll
+    for (int m = 0; m < SPT; ++m) {
+        const int n = threadIdx.x + BW * m;
+        const int64_t i = s + n;
+        double2 acc = make_double2(0.0, 0.0);
+        if (i >= 0 && i < a.T) {
+#pragma unroll
+            for (int r = 0; r < NBT; ++r) {
+                const double2 w = cmul(widen(win.v[r][m]), tone);
+                acc.x += w.x; acc.y += w.y;
+            }
+            acc.x /= (double)NBT; acc.y /= (double)NBT;                 // np.mean over branches
+        }
+        buf[rb + bitrev(BW * m, LB)] = acc;                           // bit sets of tid and BW·m disjoint
+        tone = cmul(tone, step);
+    }
+    lds_barrier();
+}
+
+// ---- fast path: N = SPT·BW, NBT branches, cp <= 2·BW, n_used <= UPT·BW (compile time) ---------
+// Against the generic kernel below (r03q/r03r: a frame waited ~40 % of its time on serialized
+// HBM round trips, and its 77 KB of LDS held the CU at 2 workgroups):
+//  * each window's nb·SPT loads per thread (and the CP correlation's) are issued together into
+//    registers (raw input words) before the first is used: one round trip per window;
+//  * the channel estimate h and the equalised xhat never leave registers: thread t owns the used
+//    bins u = t + BW·j in the LS, EQ and EVM loops alike, so only the phases (unwrap: cross-bin)
+//    go to LDS;
+//  * the twiddle table holds N/4 entries (w^{j+N/4} = -i·w^j);
+// so a workgroup needs N·16 + N/4·16 + n_used·8 bytes of LDS (50 KB at N = 2048): 3 per CU.
+// OFS_BE_FAST=0 selects the generic kernel (A/B).
+#ifndef OFS_BE_TIMING
+#define OFS_BE_TIMING 0            // diagnostic builds: per-phase cycles (tools/be_phase.py)
+#endif
+#if OFS_BE_TIMING
+__device__ unsigned long long be_prof[12];
+#define BE_T(i)                                                                                      \
+    if (threadIdx.x == 0) { const long long t_ = __builtin_amdgcn_s_memtime(); tacc[i] += t_ - tprev; tprev = t_; }
+#else
+#define BE_T(i)
+#endif
+
+__device__ __forceinline__ double2 twq_at(const double2* twq, int j, int Q) {
+    if (j < Q) return twq[j];
+    const double2 v = twq[j - Q];
+    return make_double2(v.y, -v.x);                          // w^{j} = -i·w^{j-N/4}
+}
+
+// fft_lds with the quarter twiddle table (same butterflies, same order)
+__device__ void fft_lds_q(double2* buf, const double2* twq, int N, int LB) {
+    const int Q = N / 4;
+    int len = 2;
+    if (LB & 1) {
+        for (int j = threadIdx.x; j < N / 2; j += BW) {
+            const double2 u = buf[2 * j], v = buf[2 * j + 1];
+            const double2 t = cmul(twq[0], v);
+            buf[2 * j] = make_double2(u.x + t.x, u.y + t.y);
+            buf[2 * j + 1] = make_double2(u.x - t.x, u.y - t.y);
+        }
+        lds_barrier();
+        len = 4;
+    }
+    for (; len <= N; len <<= 2) {
+        const int h = len >> 1;
+        const int s1 = N / len, s2 = N / (2 * len);
+        for (int j = threadIdx.x; j < N / 4; j += BW) {
+            const int g = j / h, k = j - g * h;
+            const int p = g * 4 * h + k;
+            const double2 a0 = buf[p], a1 = buf[p + h], a2 = buf[p + 2 * h], a3 = buf[p + 3 * h];
+            const double2 w1 = twq_at(twq, k * s1, Q);
+            const double2 t1 = cmul(w1, a1), t3 = cmul(w1, a3);
+            const double2 b0 = make_double2(a0.x + t1.x, a0.y + t1.y), b1 = make_double2(a0.x - t1.x, a0.y - t1.y);
+            const double2 b2 = make_double2(a2.x + t3.x, a2.y + t3.y), b3 = make_double2(a2.x - t3.x, a2.y - t3.y);
+            const double2 u = cmul(twq_at(twq, k * s2, Q), b2), v = cmul(twq_at(twq, (k + h) * s2, Q), b3);
+            buf[p] = make_double2(b0.x + u.x, b0.y + u.y);
+            buf[p + 2 * h] = make_double2(b0.x - u.x, b0.y - u.y);
+            buf[p + h] = make_double2(b1.x + v.x, b1.y + v.y);
+            buf[p + 3 * h] = make_double2(b1.x - v.x, b1.y - v.y);
+        }
+        lds_barrier();
+    }
+}
+
+// NV block-wide sums with one pair of barriers: DPP wave sums (inclusive scan, lane 63), then the
+// BW/64 wave totals through LDS; every thread gets the NV results.
+template <int NV>
+__device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = ofs::readlane(ofs::wave_scan_add(v[i], lane), 63);
+    lds_barrier();                                           // red's previous readers are done
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < BW / 64; ++k) t += red[k * NV + i];
+        v[i] = t;
+    }
+}
+
+// estimate_timing_offset_from_phase_slope (core.py:443-469) on ph[0..U) = angle(h) in LDS, with the
+// frame-invariant bin statistics precomputed (kmean, Σ kz, Σ kz² + 1e-12; kz = k - kmean): np.unwrap
+// as in unwrap_slope, the fit's two sums Σ phi and Σ kz·phi accumulated while each thread rewrites its
+// run, one reduction; slope = (Σ kz·phi - mean(phi)·Σ kz) / (Σ kz² + 1e-12)  (= Σ kz·(phi - mean) / ...).
+__device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U, double kmean, double skz, double den,
+                                    double* red, double* scan_tot) {
+    const int per = (U + BW - 1) / BW;
+    const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
+    double local = 0.0;
+    for (int u = max(u0, 1); u < u1; ++u) {
+        const double dd = ph[u] - ph[u - 1];
+        if (!(fabs(dd) < M_PI)) {
+            double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+            if (dm == -M_PI && dd > 0.0) dm = M_PI;
+            local += dm - dd;
+        }
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const double incl = ofs::wave_scan_add(local, lane);
+    if (lane == 63) scan_tot[w] = incl;
+    lds_barrier();
+    double run = incl - local;
+    for (int k = 0; k < w; ++k) run += scan_tot[k];
+    double prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
+    double sv[2] = {0.0, 0.0};                               // Σ phi, Σ kz·phi
+    for (int u = u0; u < u1; ++u) {
+        const double raw = ph[u];
+        if (u >= 1) {
+            const double dd = raw - prev_raw;
+            if (!(fabs(dd) < M_PI)) {
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                run += dm - dd;
+            }
+        }
+        prev_raw = raw;
+        const double phi = raw + run;
+        sv[0] += phi;
+        sv[1] += ((double)bins[u] - kmean) * phi;
+    }
+    block_sums<2>(sv, red);
+    const double pmean = sv[0] / (double)U;
+    return (sv[1] - pmean * skz) / den;
+}
+
+#ifndef OFS_BE_MINWG
+#define OFS_BE_MINWG 2             // workgroups per CU the register budget is cut for (r03s: 2 beats
+                                   // 3 - 1.21 vs 1.29 ms - the 168-VGPR cut spills)
+#endif
+template <int FMT, int SPT, int NBT, int UPT>
+__global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArgs a) {
+#if OFS_BE_TIMING
+    long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    long long tprev = __builtin_amdgcn_s_memtime();
+#endif
+    extern __shared__ __attribute__((aligned(16))) double2 bsm[];
+    __shared__ double red[4 * (BW / 64)];
+    __shared__ double scan_tot[BW / 64];
+    constexpr int N = SPT * BW;
+    double2* buf = bsm;                       // N
+    double2* twq = bsm + N;                   // N / 4
+    double* ph = reinterpret_cast<double*>(twq + N / 4);   // n_used: phase / unwrap
+    const int U = a.n_used, LB = 31 - __clz(N);
+    for (int j = threadIdx.x; j < N / 4; j += BW) {
+        double sn, cs;
+        sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
+        twq[j] = make_double2(cs, sn);
+    }
+    int kb[UPT];                              // this thread's used bins u = tid + BW·j, as X indices
+    double bsum[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+        const int u = threadIdx.x + BW * j;
+        int k = u < U ? a.bins[u] % N : 0;
+        kb[j] = k < 0 ? k + N : k;
+        if (u < U) bsum[0] += (double)a.bins[u];
+    }
+    // the phase-slope fit's frame-invariant sums (np.mean(k), Σ kz, Σ kz² + 1e-12)
+    block_sums<1>(bsum, red);
+    const double kmean = bsum[0] / (double)U;
+    double kst[2] = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+        const int u = threadIdx.x + BW * j;
+        if (u < U) {
+            const double kz = (double)a.bins[u] - kmean;
+            kst[0] += kz;
+            kst[1] += kz * kz;
+        }
+    }
+    block_sums<2>(kst, red);
+    const double skz = kst[0], kden = kst[1] + 1e-12;
+    for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    lds_barrier();
+    const int64_t ps = a.pilot_start[b], ds = a.data_start[b];
+    BeWindow<FMT, SPT, NBT> pwin;
+    BeCp<FMT, NBT> cpx;
+    pwin.issue(a, b, ps + a.cp);
+    cpx.issue(a, b, ps);
+    double cfo;
+    if (a.cfo_in) {
+        cfo = a.cfo_in[b];
+    } else {
+        double pp[2] = {0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < NBT; ++r)
+#pragma unroll
+            for (int m = 0; m < BE_CPT; ++m) {
+                const double2 u = widen(cpx.u[r][m]), v = widen(cpx.w[r][m]);
+                pp[0] += u.x * v.x + u.y * v.y;
+                pp[1] += u.y * v.x - u.x * v.y;
+            }
+        block_sums<2>(pp, red);
+        cfo = -atan2(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
+    }
+    if (a.cfo_out && threadIdx.x == 0) a.cfo_out[b] = cfo;
+    const double2* pil = a.pilot + b * a.pilot_stride;
+    const double2* dat = a.data + b * a.data_stride;
+    BE_T(0)
+    // ---- pilot: FFT, used bins, LS estimate ----
+    place_window<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, LB);
+    BE_T(1)
+    fft_lds_q(buf, twq, N, LB);
+    BE_T(2)
+    double2 hx[UPT];                                                  // h, later xhat
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+        const int u = threadIdx.x + BW * j;
+        hx[j] = make_double2(0.0, 0.0);
+        if (u < U) {
+            const double2 p = pil[u];
+            const double2 h = cdiv(buf[kb[j]], make_double2(p.x + 1e-9, p.y));   // y / (x + eps)
+            hx[j] = h;
+            ph[u] = atan2(h.y, h.x);
+            if (a.h_out) a.h_out[b * U + u] = h;
+        }
+    }
+    lds_barrier();
+    BE_T(3)
+    const double slope = unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, red, scan_tot);
+    if (threadIdx.x == 0) {
+        if (a.slope_out) a.slope_out[b] = slope;
+        if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
+    }
+    BE_T(4)
+    // ---- data: FFT, equalise, complex-gain alignment, EVM ----
+    {
+        BeWindow<FMT, SPT, NBT> dwin;
+        dwin.issue(a, b, ds + a.cp);
+        place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
+    }
+    BE_T(5)
+    fft_lds_q(buf, twq, N, LB);
+    BE_T(6)
+    double gs[4] = {0.0, 0.0, 0.0, 0.0};                              // vdot(xhat, ref), |xhat|², |ref|²
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+        const int u = threadIdx.x + BW * j;
+        if (u < U) {
+            const double2 h = hx[j];
+            const double2 xh = cdiv(buf[kb[j]], make_double2(h.x + 1e-9, h.y));   // equalize
+            hx[j] = xh;
+            const double2 r = dat[u];
+            gs[0] += xh.x * r.x + xh.y * r.y;
+            gs[1] += xh.x * r.y - xh.y * r.x;
+            gs[2] += xh.x * xh.x + xh.y * xh.y;
+            gs[3] += r.x * r.x + r.y * r.y;
+        }
+    }
+    block_sums<4>(gs, red);
+    const double rr = gs[3];
+    BE_T(7)
+    const double2 g = cdiv(make_double2(gs[0], gs[1]), make_double2(gs[2] + 1e-12, 0.0));
+    double ee[1] = {0.0};
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+        const int u = threadIdx.x + BW * j;
+        if (u < U) {
+            const double2 xa = cmul(hx[j], g);
+            if (a.xa_out) a.xa_out[b * U + u] = xa;
+            const double2 r = dat[u];
+            const double er = xa.x - r.x, ei = xa.y - r.y;
+            ee[0] += er * er + ei * ei;
+        }
+    }
+    block_sums<1>(ee, red);
+    if (threadIdx.x == 0) {
+        const double evm = sqrt((ee[0] / (double)U) / (rr / (double)U));
+        if (a.gain_out) a.gain_out[b] = g;
+        if (a.evm_out) a.evm_out[b] = evm;
+        if (a.evm_db_out) a.evm_db_out[b] = 20.0 * log10(evm + 1e-12);
+    }
+    BE_T(8)
+    }
+#if OFS_BE_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 9; ++i) atomicAdd(&be_prof[i], (unsigned long long)tacc[i]);
+#endif
 }
 
 template <int FMT>
@@ -362,6 +745,41 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BW), lds, st, a);
         return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
     };
+    const char* fe = getenv("OFS_BE_FAST");                 // 0: the generic kernel (A/B)
+    const bool fast = !(fe && atoi(fe) == 0) && (n_br == 1 || n_br == 2) && cp_len <= 2 * BW &&
+                      ((n_fft == 4 * BW && n_used <= 3 * BW) || (n_fft == 8 * BW && n_used <= 5 * BW) ||
+                       (n_fft == 16 * BW && n_used <= 10 * BW));
+    if (fast) {
+        const size_t lds_f = (size_t)n_fft * 16 + (size_t)(n_fft / 4) * 16 + (size_t)n_used * 8;
+        auto launch_f = [&](auto kern) -> int32_t {
+            if (lds_f > 64 * 1024 &&
+                hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
+                return OFS_EHIP;
+            int dev = 0, cus = 256, per = 1;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, BW, lds_f) != hipSuccess)
+                return OFS_EHIP;
+            const int64_t grid = std::min<int64_t>(B, (int64_t)cus * std::max(per, 1));
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BW), lds_f, st, a);
+            return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+        };
+#define BE_FAST(F)                                                                                   \
+        switch (n_fft / BW * 10 + n_br) {                                                            \
+            case 41: return launch_f(rx_backend_fast_kernel<F, 4, 1, 3>);                            \
+            case 42: return launch_f(rx_backend_fast_kernel<F, 4, 2, 3>);                            \
+            case 81: return launch_f(rx_backend_fast_kernel<F, 8, 1, 5>);                            \
+            case 82: return launch_f(rx_backend_fast_kernel<F, 8, 2, 5>);                            \
+            case 161: return launch_f(rx_backend_fast_kernel<F, 16, 1, 10>);                         \
+            case 162: return launch_f(rx_backend_fast_kernel<F, 16, 2, 10>);                         \
+        }
+        switch (in_fmt) {
+            case OFS_C64: BE_FAST(OFS_C64) break;
+            case OFS_C128: BE_FAST(OFS_C128) break;
+            default: BE_FAST(OFS_CI16) break;
+        }
+#undef BE_FAST
+    }
     switch (in_fmt) {
         case OFS_C64: return launch(rx_backend_kernel<OFS_C64>);
         case OFS_C128: return launch(rx_backend_kernel<OFS_C128>);
@@ -656,3 +1074,12 @@ int32_t ofs_quantize_adc(int32_t in_fmt, const void* x, int64_t n, double full_s
 }
 
 }  // extern "C"
+
+#if OFS_BE_TIMING
+// per-phase cycle totals of the fast back-end kernel since the last call (diagnostic builds)
+extern "C" int ofs_be_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(be_prof), 9 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[12] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(be_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
