@@ -463,6 +463,113 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
 #define OFS_BE_MINWG 2             // workgroups per CU the register budget is cut for (r03s: 2 beats
                                    // 3 - 1.21 vs 1.29 ms - the 168-VGPR cut spills)
 #endif
+// Radix-R DIT pass over groups of R·h (R = 2, 4, 8: log2 R radix-2 stages in registers): thread j
+// takes the R elements p + i·h of group g = j / h, k = j mod h, and applies the stages of spans h,
+// 2h, ... with the twiddles w^{(k + q·h)·N/(2·span)} - exactly the radix-2 stages' operations in
+// their order (bit-identical to fft_lds), one LDS round trip and one barrier per log2 R stages.
+template <int R>
+__device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int N, int h) {
+    const int Q = N / 4;
+    for (int j = threadIdx.x; j < N / R; j += BW) {
+        const int g = j / h, k = j - g * h;
+        const int p = g * R * h + k;
+        double2 v[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = buf[p + i * h];
+#pragma unroll
+        for (int sp = 1; sp < R; sp <<= 1) {
+            const int str = N / (2 * sp * h);
+            double2 w[R / 2];
+#pragma unroll
+            for (int q = 0; q < sp; ++q) w[q] = twq_at(twq, (k + q * h) * str, Q);
+#pragma unroll
+            for (int i0 = 0; i0 < R; i0 += 2 * sp)
+#pragma unroll
+                for (int q = 0; q < sp; ++q) {
+                    const double2 t = cmul(w[q], v[i0 + q + sp]), u = v[i0 + q];
+                    v[i0 + q] = make_double2(u.x + t.x, u.y + t.y);
+                    v[i0 + q + sp] = make_double2(u.x - t.x, u.y - t.y);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) buf[p + i * h] = v[i];
+    }
+    lds_barrier();
+}
+
+template <int B>
+__host__ __device__ constexpr int rev_bits(int v) {
+    int r = 0;
+    for (int i = 0; i < B; ++i) r |= ((v >> i) & 1) << (B - 1 - i);
+    return r;
+}
+template <int V> struct Log2 { static constexpr int value = 1 + Log2<V / 2>::value; };
+template <> struct Log2<1> { static constexpr int value = 0; };
+
+// window (registers) -> rx_eff and the FFT's first log2(SPT) stages in registers -> buf.  Thread t's
+// samples n = t + BW·m sit at bit-reversed positions rev(t)·SPT + rev(m): one whole group of the
+// h = 1 pass, so those stages (twiddles w^{q·N/(2s)}) need no LDS round trip; the remaining 8
+// stages run as radix-8, radix-8, radix-4 passes (fft_rest).
+template <int FMT, int SPT, int NBT>
+__device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, double cfo,
+                                                 const BeWindow<FMT, SPT, NBT>& win, double2* buf,
+                                                 const double2* twq) {
+    constexpr int N = SPT * BW, LS = Log2<SPT>::value;
+    const double w0 = 2.0 * M_PI * (-cfo);
+    double sn, cs, ss, cc;
+    sincos(w0 * (double)(s + (int64_t)threadIdx.x) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    sincos(w0 * (double)BW / a.fs, &ss, &cc);
+    double2 tone = make_double2(cs, sn);
+    const double2 step = make_double2(cc, ss);
+    double2 v[SPT];
+#pragma unroll
+    for (int m = 0; m < SPT; ++m) {
+        const int64_t i = s + threadIdx.x + BW * m;
+        double2 acc = make_double2(0.0, 0.0);
+        if (i >= 0 && i < a.T) {
+#pragma unroll
+            for (int r = 0; r < NBT; ++r) {
+                const double2 w = cmul(widen(win.v[r][m]), tone);
+                acc.x += w.x; acc.y += w.y;
+            }
+            acc.x /= (double)NBT; acc.y /= (double)NBT;                 // np.mean over branches
+        }
+        v[rev_bits<LS>(m)] = acc;
+        tone = cmul(tone, step);
+    }
+#pragma unroll
+    for (int sp = 1; sp < SPT; sp <<= 1) {                              // h = 1, k = 0
+#pragma unroll
+        for (int i0 = 0; i0 < SPT; i0 += 2 * sp)
+#pragma unroll
+            for (int q = 0; q < sp; ++q) {
+                const double2 w = twq_at(twq, q * (N / (2 * sp)), N / 4);
+                const double2 t = cmul(w, v[i0 + q + sp]), u = v[i0 + q];
+                v[i0 + q] = make_double2(u.x + t.x, u.y + t.y);
+                v[i0 + q + sp] = make_double2(u.x - t.x, u.y - t.y);
+            }
+    }
+    double2* dst = buf + bitrev(threadIdx.x, 8) * SPT;
+#pragma unroll
+    for (int i = 0; i < SPT; ++i) dst[i] = v[i];
+    lds_barrier();
+}
+
+template <int SPT>
+__device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
+    constexpr int N = SPT * BW;
+    fft_pass<8>(buf, twq, N, SPT);
+    fft_pass<8>(buf, twq, N, 8 * SPT);
+    fft_pass<4>(buf, twq, N, 64 * SPT);
+}
+
+#ifndef OFS_BE_PF
+#define OFS_BE_PF 1                // 0: each frame's pilot window / CP loads issued at its start (A/B)
+#endif
+#ifndef OFS_BE_R8
+#define OFS_BE_R8 1                // 0: place_window + fft_lds_q (A/B)
+#endif
+
 template <int FMT, int SPT, int NBT, int UPT>
 __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArgs a) {
 #if OFS_BE_TIMING
@@ -477,6 +584,8 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     double2* twq = bsm + N;                   // N / 4
     double* ph = reinterpret_cast<double*>(twq + N / 4);   // n_used: phase / unwrap
     const int U = a.n_used, LB = 31 - __clz(N);
+    constexpr bool R8 = OFS_BE_R8 && SPT <= 8;           // 16 samples per thread in registers would spill
+    constexpr bool PF = OFS_BE_PF && SPT <= 8 && sizeof(typename BeRaw<FMT>::T) <= 8;   // (complex128 too)
     for (int j = threadIdx.x; j < N / 4; j += BW) {
         double sn, cs;
         sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
@@ -506,13 +615,19 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     }
     block_sums<2>(kst, red);
     const double skz = kst[0], kden = kst[1] + 1e-12;
+    BeWindow<FMT, SPT, NBT> pwin;
+    BeCp<FMT, NBT> cpx;
+    if (PF && blockIdx.x < a.B) {
+        pwin.issue(a, blockIdx.x, a.pilot_start[blockIdx.x] + a.cp);
+        cpx.issue(a, blockIdx.x, a.pilot_start[blockIdx.x]);
+    }
     for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     lds_barrier();
     const int64_t ps = a.pilot_start[b], ds = a.data_start[b];
-    BeWindow<FMT, SPT, NBT> pwin;
-    BeCp<FMT, NBT> cpx;
-    pwin.issue(a, b, ps + a.cp);
-    cpx.issue(a, b, ps);
+    if (!PF) {
+        pwin.issue(a, b, ps + a.cp);
+        cpx.issue(a, b, ps);
+    }
     double cfo;
     if (a.cfo_in) {
         cfo = a.cfo_in[b];
@@ -534,9 +649,15 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     const double2* dat = a.data + b * a.data_stride;
     BE_T(0)
     // ---- pilot: FFT, used bins, LS estimate ----
-    place_window<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, LB);
-    BE_T(1)
-    fft_lds_q(buf, twq, N, LB);
+    if constexpr (R8) {
+        place_window_fft<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, twq);
+        BE_T(1)
+        fft_rest<SPT>(buf, twq);
+    } else {
+        place_window<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, LB);
+        BE_T(1)
+        fft_lds_q(buf, twq, N, LB);
+    }
     BE_T(2)
     double2 hx[UPT];                                                  // h, later xhat
 #pragma unroll
@@ -561,12 +682,19 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     BE_T(4)
     // ---- data: FFT, equalise, complex-gain alignment, EVM ----
     {
-        BeWindow<FMT, SPT, NBT> dwin;
-        dwin.issue(a, b, ds + a.cp);
-        place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
+        BeWindow<FMT, SPT, NBT> dwin;                                 // (issued during the pilot's work instead:
+        dwin.issue(a, b, ds + a.cp);                                  // r03w, 1.00 vs 0.97 ms - registers)
+        if constexpr (R8) place_window_fft<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, twq);
+        else place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
+    }
+    if (PF && b + gridDim.x < a.B) {                           // the next frame's pilot window and
+        const int64_t bn = b + gridDim.x;                             // CP samples land during this frame's
+        pwin.issue(a, bn, a.pilot_start[bn] + a.cp);                  // data FFT, EQ and EVM
+        cpx.issue(a, bn, a.pilot_start[bn]);
     }
     BE_T(5)
-    fft_lds_q(buf, twq, N, LB);
+    if constexpr (R8) fft_rest<SPT>(buf, twq);
+    else fft_lds_q(buf, twq, N, LB);
     BE_T(6)
     double gs[4] = {0.0, 0.0, 0.0, 0.0};                              // vdot(xhat, ref), |xhat|², |ref|²
 #pragma unroll

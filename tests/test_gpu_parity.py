@@ -522,8 +522,11 @@ def test_receiver_backend_vs_reference_golden(name):
     assert np.allclose(out["evm"].cpu().numpy(), float(d["evm"]), rtol=1e-9)
 
 
-@pytest.mark.parametrize("fmt,nb,N", [("c64", 1, 2048), ("int16", 2, 1024), ("c128", 3, 256)])
-def test_receiver_backend_batched_vs_oracle(fmt, nb, N):
+@pytest.mark.parametrize("fmt,nb,N", [("c64", 1, 2048), ("int16", 2, 1024), ("c128", 3, 256), ("c64", 2, 4096),
+                                      ("c128", 2, 2048)])
+def test_receiver_backend_batched_vs_oracle(fmt, nb, N, monkeypatch):
+    """The fused back-end (fast kernel for N = 1024 / 2048 / 4096 and 1-2 branches, the generic one
+    otherwise and under OFS_BE_FAST=0) against the oracle's chain, per frame."""
     rng = np.random.default_rng(N + nb)
     B, cp = 6, N // 4
     k = core.centered_subcarrier_indices(N // 2)
@@ -539,12 +542,17 @@ def test_receiver_backend_batched_vs_oracle(fmt, nb, N):
     else:
         xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
     out = core.receiver_backend_batched(xd, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
+    monkeypatch.setenv("OFS_BE_FAST", "0")
+    gen = core.receiver_backend_batched(xd, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
+    monkeypatch.delenv("OFS_BE_FAST")
     for b in range(B):
         r = O.rx_backend(x[b], int(ps[b]), int(ds[b]), N, cp, 1e6, k, pil[b], dat)
-        assert abs(out["cfo"][b].item() - r["cfo"]) < 1e-6
-        assert relerr(out["h"][b].cpu().numpy(), r["h"]) < 1e-9
-        assert relerr(out["xa"][b].cpu().numpy(), r["xa"]) < 1e-8
-        assert abs(out["evm"][b].item() - r["evm"]) < 1e-8 * max(1.0, r["evm"])
+        for o in (out, gen):
+            assert abs(o["cfo"][b].item() - r["cfo"]) < 1e-6
+            assert relerr(o["h"][b].cpu().numpy(), r["h"]) < 1e-9
+            assert relerr(o["xa"][b].cpu().numpy(), r["xa"]) < 1e-8
+            assert abs(o["evm"][b].item() - r["evm"]) < 1e-8 * max(1.0, r["evm"])
+            assert abs(o["slope"][b].item() - r["slope"]) < 1e-9 * max(1.0, abs(r["slope"]))
 
 
 @pytest.mark.parametrize("T,L", [(1024, 512), (1024, 128), (768, 256)])
