@@ -19,6 +19,7 @@
 #include <math.h>
 #include <mutex>
 #include <algorithm>
+#include <cstdlib>
 #include "ofdmsync.h"
 
 namespace {
@@ -34,6 +35,7 @@ struct McPlan {
     int32_t N = 0, M = 0, S = 0, nb = 0;
     int64_t B = 0, T = 0, nblk = 0, nout = 0;
     double2* H = nullptr;           // [M] FFT of the reversed conjugated reference
+    double2* Hbr = nullptr;         // fused path (M = MF_M): H[bitrev(i)] / M
     double ref_norm = 0.0;
     size_t work_bytes = 0;
     size_t scratch_bytes = 0;
@@ -79,6 +81,202 @@ __global__ __launch_bounds__(FW) void mc_mul_kernel(double2* U, const double2* H
         const double2 u = U[i], h = H[i % M];
         U[i] = make_double2((u.x * h.x - u.y * h.y) * scale, (u.x * h.y + u.y * h.x) * scale);
     }
+}
+
+// ---- fused overlap-save block (M = MF_M = 8192): pack + FFT + ·H/M + inverse FFT in one kernel ----
+// One 1024-thread workgroup per (row, block), the block in LDS (128 KiB), never in HBM between the
+// transforms (the rocFFT path writes and reads the [rows·nblk][M] scratch four times, plus pack and
+// multiply passes).  Forward: decimation in frequency, natural order in -> bit-reversed order out, so
+// the pointwise product uses H in bit-reversed order (Hbr, built with the plan) and needs no
+// reordering; inverse = conj(DFT(conj(·))), a decimation-in-time DFT: bit-reversed in -> natural out.
+// Thread t holds samples t + 1024·m (m < 8): the three largest-span stages of each transform run in
+// registers (the load / the final store), the other ten as radix-8, radix-8, radix-4, radix-4 LDS
+// passes.  Twiddles w^j (w = e^{-2 pi i/M}) from two 64-entry LDS tables; the block sits in LDS with
+// one pad per 16 elements (141 KiB per workgroup).  Only the valid outputs m >= N-1 are written to
+// the scratch the extract kernel reads.  512 x 16384 c128, 2048 taps: pack + rocFFT + multiply +
+// rocFFT (~305 us) -> 160-173 us; the whole matched filter 0.52 -> 0.37 ms (profiles/r03z*).
+constexpr int MF_T = 1024;
+constexpr int MF_M = 8 * MF_T;
+
+// twiddle w^e, e < M/2, from two 64-entry LDS tables: w^e = w^{64·(e>>6)} · w^{e & 63} (one complex
+// product, ~1 ulp more than a full table; the full quarter table would not fit beside the block)
+__device__ __forceinline__ double2 mf_tw(const double2* tws, int e) {
+    const double2 a = tws[64 + (e >> 6)], b = tws[e & 63];
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// LDS position of block element e: one 16-byte pad per 16 elements, so the radix passes with small
+// spans (elements 4 or 16 apart in consecutive lanes) spread over the banks
+__device__ __forceinline__ int mf_at(int e) { return e + (e >> 4); }
+constexpr int MF_LDS = (MF_M + MF_M / 16 + 128) * 16;     // padded block + the two twiddle tables
+__device__ __forceinline__ double2 mf_mul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ void mf_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// DIF radix-R pass over spans (R/2)h .. h; LAST: then ·Hbr and conjugate (the inverse's input)
+template <int R, bool LAST>
+__device__ __forceinline__ void mf_dif(double2* fb, const double2* twq, int h, const double2* __restrict__ Hbr) {
+    for (int j = threadIdx.x; j < MF_M / R; j += MF_T) {
+        const int g = j / h, k = j - g * h;
+        const int p = g * R * h + k;
+        double2 v[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = fb[mf_at(p + i * h)];
+#pragma unroll
+        for (int sp = R / 2; sp >= 1; sp >>= 1) {
+            const int str = MF_M / (2 * sp * h);
+            double2 w[R / 2];
+#pragma unroll
+            for (int q = 0; q < sp; ++q) w[q] = mf_tw(twq, (k + q * h) * str);
+#pragma unroll
+            for (int i0 = 0; i0 < R; i0 += 2 * sp)
+#pragma unroll
+                for (int q = 0; q < sp; ++q) {
+                    const double2 a = v[i0 + q], b = v[i0 + q + sp];
+                    v[i0 + q] = make_double2(a.x + b.x, a.y + b.y);
+                    v[i0 + q + sp] = mf_mul(make_double2(a.x - b.x, a.y - b.y), w[q]);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            if (LAST) {
+                const double2 y = mf_mul(v[i], Hbr[p + i * h]);
+                v[i] = make_double2(y.x, -y.y);
+            }
+            fb[mf_at(p + i * h)] = v[i];
+        }
+    }
+    mf_sync();
+}
+// DIT radix-R pass over spans h .. (R/2)h
+template <int R>
+__device__ __forceinline__ void mf_dit(double2* fb, const double2* twq, int h) {
+    for (int j = threadIdx.x; j < MF_M / R; j += MF_T) {
+        const int g = j / h, k = j - g * h;
+        const int p = g * R * h + k;
+        double2 v[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = fb[mf_at(p + i * h)];
+#pragma unroll
+        for (int sp = 1; sp < R; sp <<= 1) {
+            const int str = MF_M / (2 * sp * h);
+            double2 w[R / 2];
+#pragma unroll
+            for (int q = 0; q < sp; ++q) w[q] = mf_tw(twq, (k + q * h) * str);
+#pragma unroll
+            for (int i0 = 0; i0 < R; i0 += 2 * sp)
+#pragma unroll
+                for (int q = 0; q < sp; ++q) {
+                    const double2 t = mf_mul(w[q], v[i0 + q + sp]), u = v[i0 + q];
+                    v[i0 + q] = make_double2(u.x + t.x, u.y + t.y);
+                    v[i0 + q + sp] = make_double2(u.x - t.x, u.y - t.y);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i) fb[mf_at(p + i * h)] = v[i];
+    }
+    mf_sync();
+}
+
+template <int FMT>
+__global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2* __restrict__ Hbr) {
+    extern __shared__ __attribute__((aligned(16))) double2 fb[];     // [MF_M + pads], then 2 x 64 twiddles
+    const int t = threadIdx.x;
+    double2* tws = fb + MF_M + MF_M / 16;
+    if (t < 128) {                                                    // w^l, l < 64; w^{64h}, h < 64
+        double sn, cs;
+        sincospi(-2.0 * (double)(t < 64 ? t : 64 * (t - 64)) / (double)MF_M, &sn, &cs);
+        tws[t] = make_double2(cs, sn);
+    }
+    mf_sync();
+    const double2* twq = tws;
+    const int64_t blk = blockIdx.x;                                   // row·nblk + q
+    const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+    const int64_t g0 = q * a.S - (a.N - 1);
+    double2 v[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int64_t g = g0 + t + MF_T * m;
+        v[m] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, row * a.T + g) : make_double2(0.0, 0.0);
+    }
+    // forward DIF, spans 4096, 2048, 1024 (twiddle exponents offset·M/(2·span))
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const double2 x0 = v[m], x1 = v[m + 4];
+        v[m] = make_double2(x0.x + x1.x, x0.y + x1.y);
+        v[m + 4] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, t + MF_T * m));
+    }
+#pragma unroll
+    for (int m = 0; m < 8; m += 4)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const double2 x0 = v[m + r], x1 = v[m + r + 2];
+            v[m + r] = make_double2(x0.x + x1.x, x0.y + x1.y);
+            v[m + r + 2] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, 2 * (t + MF_T * r)));
+        }
+#pragma unroll
+    for (int m = 0; m < 8; m += 2) {
+        const double2 x0 = v[m], x1 = v[m + 1];
+        v[m] = make_double2(x0.x + x1.x, x0.y + x1.y);
+        v[m + 1] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, 4 * t));
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) fb[mf_at(t + MF_T * m)] = v[m];
+    mf_sync();
+    mf_dif<8, false>(fb, twq, 128, Hbr);                             // spans 512, 256, 128
+    mf_dif<8, false>(fb, twq, 16, Hbr);                              // 64, 32, 16
+    mf_dif<4, false>(fb, twq, 4, Hbr);                               // 8, 4
+    mf_dif<4, true>(fb, twq, 1, Hbr);                                // 2, 1; then conj(X·H/M)
+    mf_dit<4>(fb, twq, 1);                                           // spans 1, 2
+    mf_dit<4>(fb, twq, 4);                                           // 4, 8
+    mf_dit<8>(fb, twq, 16);                                          // 16, 32, 64
+    mf_dit<8>(fb, twq, 128);                                         // 128, 256, 512
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = fb[mf_at(t + MF_T * m)];
+#pragma unroll
+    for (int m = 0; m < 8; m += 2) {                                 // span 1024
+        const double2 tt = mf_mul(mf_tw(twq, 4 * t), v[m + 1]), u = v[m];
+        v[m] = make_double2(u.x + tt.x, u.y + tt.y);
+        v[m + 1] = make_double2(u.x - tt.x, u.y - tt.y);
+    }
+#pragma unroll
+    for (int m = 0; m < 8; m += 4)                                   // span 2048
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const double2 tt = mf_mul(mf_tw(twq, 2 * (t + MF_T * r)), v[m + r + 2]), u = v[m + r];
+            v[m + r] = make_double2(u.x + tt.x, u.y + tt.y);
+            v[m + r + 2] = make_double2(u.x - tt.x, u.y - tt.y);
+        }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {                                    // span 4096
+        const double2 tt = mf_mul(mf_tw(twq, t + MF_T * m), v[m + 4]), u = v[m];
+        v[m] = make_double2(u.x + tt.x, u.y + tt.y);
+        v[m + 4] = make_double2(u.x - tt.x, u.y - tt.y);
+    }
+    double2* dst = a.U + blk * (int64_t)MF_M;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const int o = t + MF_T * m;
+        if (o >= a.N - 1) dst[o] = make_double2(v[m].x, -v[m].y);   // conj: the inverse transform
+    }
+}
+
+// Hbr[i] = H[bitrev(i)] / M, for the fused path
+__global__ void mc_prep_kernel(const double2* H, double2* Hbr, int M, int lb) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+        const int r = (int)(__brev((unsigned)i) >> (32 - lb));
+        const double2 h = H[r];
+        Hbr[i] = make_double2(h.x / (double)M, h.y / (double)M);
+    }
+}
+
+bool mc_fused_enabled() {                       // OFS_MC_FUSED=0: the rocFFT pipeline (A/B)
+    const char* e = getenv("OFS_MC_FUSED");
+    return !(e && atoi(e) == 0);
 }
 
 // inclusive block scan of per-thread sums (fp64), returns the exclusive prefix of this thread
@@ -259,13 +457,22 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
     // host time comparable to the whole GPU pipeline at this size)
     const size_t lds = extract_lds(p->nb, p->M);
     bool ok2 = rocfft_execution_info_create(&p->info) == rocfft_status_success;
-    if (ok2 && lds > 64 * 1024)
-        ok2 = hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds) == hipSuccess &&
-              hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_C128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds) == hipSuccess &&
-              hipFuncSetAttribute((const void*)mc_extract_kernel<OFS_CI16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds) == hipSuccess;
+    if (ok2 && p->M == MF_M) {                  // fused path resources (optional: rocFFT otherwise)
+        if (hipMalloc(&p->Hbr, (size_t)MF_M * sizeof(double2)) == hipSuccess) {
+            hipLaunchKernelGGL(mc_prep_kernel, dim3(MF_M / 256), dim3(256), 0, 0, p->H, p->Hbr, MF_M, 13);
+            const size_t fl = MF_LDS;
+            const bool okf = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_CI16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess;
+            if (!okf) {
+                (void)hipFree(p->Hbr);
+                p->Hbr = nullptr;
+            }
+        } else {
+            p->Hbr = nullptr;
+        }
+    }
     if (!ok2) {
         if (p->info) rocfft_execution_info_destroy(p->info);
         rocfft_plan_destroy(p->fwd);
@@ -287,6 +494,7 @@ int32_t ofs_zc_mf_plan_destroy(void* plan) {
     if (p->fwd) rocfft_plan_destroy(p->fwd);
     if (p->inv) rocfft_plan_destroy(p->inv);
     if (p->H) (void)hipFree(p->H);
+    if (p->Hbr) (void)hipFree(p->Hbr);
     delete p;
     return OFS_OK;
 }
@@ -304,6 +512,24 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
     McArgs a{x, T, n_br, p->N, p->M, p->S, p->nblk, p->nout, mode, sqrt(ref_energy), static_cast<double2*>(scratch),
              p->H, static_cast<double2*>(corr), corr_mag};
     const int64_t rows = B * n_br;
+    if (p->Hbr && mc_fused_enabled() && rows * p->nblk <= 0x7fffffff) {
+        const dim3 gf((unsigned)(rows * p->nblk));
+        const size_t fl = MF_LDS;
+        switch (in_fmt) {
+            case OFS_C64: hipLaunchKernelGGL(mc_fused_kernel<OFS_C64>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
+            case OFS_C128: hipLaunchKernelGGL(mc_fused_kernel<OFS_C128>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
+            default: hipLaunchKernelGGL(mc_fused_kernel<OFS_CI16>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
+        }
+        if (hipGetLastError() != hipSuccess) return OFS_EHIP;
+        const size_t lds = extract_lds(n_br, p->M);
+        const dim3 ge((unsigned)p->nblk, (unsigned)B);
+        switch (in_fmt) {
+            case OFS_C64: hipLaunchKernelGGL(mc_extract_kernel<OFS_C64>, ge, dim3(FX), lds, st, a); break;
+            case OFS_C128: hipLaunchKernelGGL(mc_extract_kernel<OFS_C128>, ge, dim3(FX), lds, st, a); break;
+            default: hipLaunchKernelGGL(mc_extract_kernel<OFS_CI16>, ge, dim3(FX), lds, st, a); break;
+        }
+        return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+    }
     const dim3 gp((unsigned)((p->M + FW - 1) / FW), (unsigned)(rows * p->nblk));
     switch (in_fmt) {
         case OFS_C64: hipLaunchKernelGGL(mc_pack_kernel<OFS_C64>, gp, dim3(FW), 0, st, a); break;

@@ -433,9 +433,11 @@ def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
 
 @pytest.mark.parametrize("fmt,nb,N,T", [("c128", 1, 2048, 16384), ("c128", 2, 2048, 7000), ("c64", 3, 1024, 3000),
                                         ("int16", 2, 512, 2500), ("c128", 1, 2048, 1000), ("c128", 2, 256, 40)])
-def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T):
+def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, monkeypatch):
     """FFT overlap-save matched filter (ofs_zc_correlate_fft) against the direct sums on the same
-    samples, every combine mode: corr within 1e-11 of the row maximum, |corr| 1e-9 relative."""
+    samples, every combine mode: corr within 1e-11 of the row maximum, |corr| 1e-9 relative; for
+    8192-point blocks both the fused LDS-FFT kernel (default) and the rocFFT pipeline
+    (OFS_MC_FUSED=0)."""
     rng = np.random.default_rng(N + T + nb)
     B = 3
     x = rng_c(rng, B, nb, T) * 100
@@ -446,13 +448,16 @@ def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T):
         xd = torch.from_numpy(np.stack([np.round(x.real), np.round(x.imag)], -1).astype(np.int16)).cuda()
     else:
         xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
-    for mode in (zc_v2.OFS_ZC_RAW, zc_v2.OFS_ZC_V2, zc_v2.OFS_ZC_COMBINED, zc_v2.OFS_ZC_SUM):
-        cf, mf = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
-        cd, md = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="direct")
-        cf, cd, mf, md = cf.cpu().numpy(), cd.cpu().numpy(), mf.cpu().numpy(), md.cpu().numpy()
-        scale = np.abs(cd).max(axis=-1, keepdims=True)
-        assert np.max(np.abs(cf - cd) / scale) < 1e-11, mode
-        np.testing.assert_allclose(mf, md, rtol=1e-9, atol=1e-11 * float(scale.max()))
+    for fused in ("1", "0"):
+        monkeypatch.setenv("OFS_MC_FUSED", fused)
+        for mode in (zc_v2.OFS_ZC_RAW, zc_v2.OFS_ZC_V2, zc_v2.OFS_ZC_COMBINED, zc_v2.OFS_ZC_SUM):
+            cf, mf = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
+            cd, md = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="direct")
+            cf, cd, mf, md = cf.cpu().numpy(), cd.cpu().numpy(), mf.cpu().numpy(), md.cpu().numpy()
+            scale = np.abs(cd).max(axis=-1, keepdims=True)
+            assert np.max(np.abs(cf - cd) / scale) < 1e-11, (mode, fused)
+            np.testing.assert_allclose(mf, md, rtol=1e-9, atol=1e-11 * float(scale.max()))
+    monkeypatch.delenv("OFS_MC_FUSED")
 
 
 def test_zc_detect_four_branches_n2048_falls_back_to_direct():
