@@ -182,7 +182,7 @@ __device__ __forceinline__ void mf_dit(double2* fb, const double2* twq, int h) {
     mf_sync();
 }
 
-template <int FMT>
+template <int FMT, bool FUSE_X>
 __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2* __restrict__ Hbr) {
     extern __shared__ __attribute__((aligned(16))) double2 fb[];     // [MF_M + pads], then 2 x 64 twiddles
     const int t = threadIdx.x;
@@ -257,11 +257,69 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
         v[m] = make_double2(u.x + tt.x, u.y + tt.y);
         v[m + 4] = make_double2(u.x - tt.x, u.y - tt.y);
     }
-    double2* dst = a.U + blk * (int64_t)MF_M;
+    if (!FUSE_X) {
+        double2* dst = a.U + blk * (int64_t)MF_M;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            const int o = t + MF_T * m;
+            if (o >= a.N - 1) dst[o] = make_double2(v[m].x, -v[m].y);   // conj: the inverse transform
+        }
+        return;
+    }
+    // ---- one branch: the extract fused in (mc_extract_kernel's arithmetic) ----
+    // window energies from an fp64 prefix of |u_q|^2 over the block, in the (now free) block LDS:
+    // thread t scans u[8t .. 8t+7] (re-read, L2), block scan of the thread totals, P[j] = Σ_{i<j}
+    mf_sync();
+    double* P = reinterpret_cast<double*>(fb);                      // [MF_M + 1] (+ per-wave totals)
+    double* wt = P + MF_M + 1;
+    double e8[8], loc = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int64_t g = g0 + 8 * t + i;
+        double e = 0.0;
+        if (g >= 0 && g < a.T) { const double2 u = ldx<FMT>(a.x, row * a.T + g); e = u.x * u.x + u.y * u.y; }
+        e8[i] = e;
+        loc += e;
+    }
+    const int lane = t & 63, wv = t >> 6;
+    double incl = loc;                                               // wave inclusive scan of the totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double o2 = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o2;
+    }
+    if (lane == 63) wt[wv] = incl;
+    mf_sync();
+    double run = incl - loc;
+    for (int k = 0; k < wv; ++k) run += wt[k];
+    if (t == 0) P[0] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { run += e8[i]; P[8 * t + i + 1] = run; }
+    mf_sync();
+    const int64_t n0 = q * a.S;
+    const int ns = (int)min((int64_t)a.S, a.nout - n0);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        const int o = t + MF_T * m;
-        if (o >= a.N - 1) dst[o] = make_double2(v[m].x, -v[m].y);   // conj: the inverse transform
+        const int o = t + MF_T * m, s = o - (a.N - 1);
+        if (s < 0 || s >= ns) continue;
+        const double2 c = make_double2(v[m].x, -v[m].y);
+        const int64_t oi = row * a.nout + n0 + s;                    // one branch: row = stream
+        if (a.mode == OFS_ZC_RAW || a.mode == OFS_ZC_SUM) {
+            if (a.out) a.out[oi] = c;
+            if (a.mag) a.mag[oi] = hypot(c.x, c.y);
+            continue;
+        }
+        const double e = P[o + 1] - P[o + 1 - a.N];                  // Σ |x|^2 over the N-sample window
+        double2 r;
+        if (a.mode == OFS_ZC_V2) {
+            const double d = a.ref_norm * sqrt(e > 1e-12 ? e : 1e-12);
+            r = make_double2(c.x / d, c.y / d);
+        } else {                                                     // OFS_ZC_COMBINED
+            const double d = a.ref_norm * sqrt((e > 0.0 ? e : 0.0) + 1e-12);
+            r = make_double2(c.x / d, c.y / d);
+        }
+        if (a.out) a.out[oi] = r;
+        if (a.mag) a.mag[oi] = hypot(r.x, r.y);
     }
 }
 
@@ -276,6 +334,10 @@ __global__ void mc_prep_kernel(const double2* H, double2* Hbr, int M, int lb) {
 
 bool mc_fused_enabled() {                       // OFS_MC_FUSED=0: the rocFFT pipeline (A/B)
     const char* e = getenv("OFS_MC_FUSED");
+    return !(e && atoi(e) == 0);
+}
+bool mc_fuse_extract() {                        // OFS_MC_FUSE_X=0: scratch + extract kernel (A/B)
+    const char* e = getenv("OFS_MC_FUSE_X");
     return !(e && atoi(e) == 0);
 }
 
@@ -462,9 +524,12 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
             hipLaunchKernelGGL(mc_prep_kernel, dim3(MF_M / 256), dim3(256), 0, 0, p->H, p->Hbr, MF_M, 13);
             const size_t fl = MF_LDS;
             const bool okf = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
-                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
-                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_CI16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess;
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_CI16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C128, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&
+                hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_CI16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess;
             if (!okf) {
                 (void)hipFree(p->Hbr);
                 p->Hbr = nullptr;
@@ -515,12 +580,18 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
     if (p->Hbr && mc_fused_enabled() && rows * p->nblk <= 0x7fffffff) {
         const dim3 gf((unsigned)(rows * p->nblk));
         const size_t fl = MF_LDS;
+        const bool fx = n_br == 1 && mc_fuse_extract();             // one branch: no scratch round trip
+#define MF_GO(F)                                                                                      \
+        if (fx) hipLaunchKernelGGL((mc_fused_kernel<F, true>), gf, dim3(MF_T), fl, st, a, p->Hbr);     \
+        else hipLaunchKernelGGL((mc_fused_kernel<F, false>), gf, dim3(MF_T), fl, st, a, p->Hbr);
         switch (in_fmt) {
-            case OFS_C64: hipLaunchKernelGGL(mc_fused_kernel<OFS_C64>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
-            case OFS_C128: hipLaunchKernelGGL(mc_fused_kernel<OFS_C128>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
-            default: hipLaunchKernelGGL(mc_fused_kernel<OFS_CI16>, gf, dim3(MF_T), fl, st, a, p->Hbr); break;
+            case OFS_C64: MF_GO(OFS_C64) break;
+            case OFS_C128: MF_GO(OFS_C128) break;
+            default: MF_GO(OFS_CI16) break;
         }
+#undef MF_GO
         if (hipGetLastError() != hipSuccess) return OFS_EHIP;
+        if (fx) return OFS_OK;
         const size_t lds = extract_lds(n_br, p->M);
         const dim3 ge((unsigned)p->nblk, (unsigned)B);
         switch (in_fmt) {
