@@ -432,7 +432,8 @@ def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
 
 
 @pytest.mark.parametrize("fmt,nb,N,T", [("c128", 1, 2048, 16384), ("c128", 2, 2048, 7000), ("c64", 3, 1024, 3000),
-                                        ("int16", 2, 512, 2500), ("c128", 1, 2048, 1000), ("c128", 2, 256, 40)])
+                                        ("int16", 2, 512, 2500), ("c128", 1, 2048, 1000), ("c128", 2, 256, 40),
+                                        ("c64", 1, 2048, 9000), ("int16", 1, 2048, 12000)])
 def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, monkeypatch):
     """FFT overlap-save matched filter (ofs_zc_correlate_fft) against the direct sums on the same
     samples, every combine mode: corr within 1e-11 of the row maximum, |corr| 1e-9 relative; for
