@@ -3,9 +3,10 @@
 // The only sequential part of zc_streaming_detection is the reference's running sum
 // (RunningSum.step, zc_v2.py:219-238): acc = (acc + c[i]) - c[i-W] in float64, left to right.
 // Its rounding does not commute, so it is evaluated exactly in that order — but by ONE LANE PER
-// STREAM: a workgroup owns ZS = 16 streams, and 16 lanes of its wave 0 (the walker) advance the 16
-// recursions together, one sample per step (2 dependent v_add_f64).  Everything else is parallel
-// over samples and runs in the other three waves of the workgroup, one chunk behind the walker:
+// STREAM: a workgroup owns ZS streams (16 on the LDS-DMA path), and ZS lanes of its wave 0 (the
+// walker) advance the ZS recursions together, one sample per step (2 dependent v_add_f64).
+// Everything else is parallel over samples and runs in the ZH helper waves of the workgroup (7 on
+// the LDS-DMA path), one chunk behind the walker:
 // the threshold flags (corr_scaled >= thresh_scaled, |c| >= min), the stores of every state
 // array (coalesced 64-sample rows), and the gate machine in closed form.
 //
@@ -30,10 +31,21 @@ using namespace ofs;
 
 namespace {
 
+// streams per workgroup (walker lanes) and helper waves: LDS-DMA path 16 streams, 7 helpers (one
+// 116 KiB workgroup of 8 waves per CU); register path 8 streams, 3 helpers (its staging registers
+// scale with the stream count)
 #ifndef OFS_ZC_S
-#define OFS_ZC_S 8
+#define OFS_ZC_S 16
 #endif
-constexpr int ZS = OFS_ZC_S;      // streams per workgroup (walker lanes)
+#ifndef OFS_ZC_H
+#define OFS_ZC_H 7
+#endif
+#ifndef OFS_ZC_S_REG
+#define OFS_ZC_S_REG 8
+#endif
+#ifndef OFS_ZC_H_REG
+#define OFS_ZC_H_REG 3
+#endif
 #ifndef OFS_ZC_R
 #define OFS_ZC_R 2
 #endif
@@ -50,7 +62,6 @@ constexpr int ZS = OFS_ZC_S;      // streams per workgroup (walker lanes)
 constexpr int ZR = OFS_ZC_R;      // 64-sample rows of the gate machine per chunk
 constexpr int ZC = 64 * ZR;       // samples per chunk
 constexpr int ZP = ZC + 2;        // LDS row pitch in doubles (16-byte rows; walker column reads spread over banks)
-constexpr int ZH = 3;             // helper waves
 
 struct ZcArgs {
     const double* mag;
@@ -73,16 +84,42 @@ struct ZGate {
 // registers), two chunks ahead of use instead of one (the register path's loads land one chunk
 // period after they are issued, so a chunk could not be shorter than a memory round trip);
 // taken when every tile row is a whole, 16-byte-aligned 1 KiB span (host checks).
-constexpr int ZDMA_PER_CHUNK = 2 * ZS * (ZC / 128);   // DMA instructions per chunk (c and c[i-W])
 
-template <bool DMA>
-__global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
+#ifndef OFS_ZC_TIMING
+#define OFS_ZC_TIMING 0            // diagnostic builds: per-role cycles (tools/zc_phase.py)
+#endif
+#if OFS_ZC_TIMING
+__device__ unsigned long long zc_prof[8];
+__device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-major), first launch rows
+#define ZC_T(i)                                                                                      \
+    if (lane == 0) { const long long t_ = __builtin_amdgcn_s_memtime(); tacc[i] += t_ - tprev; tprev = t_; }
+#else
+#define ZC_T(i)
+#endif
+#ifndef OFS_ZC_ZB
+#define OFS_ZC_ZB 8                // walker: samples per LDS batch (read one batch ahead of the adds)
+#endif
+#ifndef OFS_ZC_QUIET
+#define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
+#endif
+template <bool DMA, int ZS, int ZH>
+__global__ __launch_bounds__(64 * (1 + ZH))
+void zc_cfar_kernel(ZcArgs a) {
 #pragma clang fp contract(off)
+#if OFS_ZC_TIMING
+    long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long tprev = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096 && threadIdx.x / 64 < 8)
+        zc_hwid[blockIdx.x * 8 + threadIdx.x / 64] = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+#endif
     constexpr int NC = DMA ? 4 : 3, NO = DMA ? 3 : 2;
+    constexpr int ZDMA_PER_CHUNK = 2 * ZS * (ZC / 128);   // DMA instructions per chunk (c and c[i-W])
     __shared__ double tc[NC][ZS][ZP];     // c
     __shared__ double to[NO][ZS][ZP];     // c[i - W] (0 before the window fills)
     __shared__ double ta[2][ZS][ZP];      // running sum after sample i
     const int lane = threadIdx.x & 63;
+    // role of this wave: 0 = walker, 1..ZH = helpers.  (Choosing the walker by SIMD id, so that
+    // both workgroups of a CU put their walkers on one SIMD, measured slower: 0.38 -> 0.45 ms.)
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t b0 = (int64_t)blockIdx.x * ZS;
     const int ns = (int)min((int64_t)ZS, a.B - b0);          // streams of this workgroup
@@ -173,11 +210,15 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
             if constexpr (DMA) {
                 if (q + 2 < nch) dma(q + 2);
                 // chunk q has landed once at most the (up to two) later chunks' DMAs are in flight
-                static_assert(ZDMA_PER_CHUNK == 16, "vmcnt immediates below assume 16 DMAs per chunk");
+                // (loads complete in order, so "at most min(63, later x per-chunk) outstanding"
+                // implies chunk q has landed; 63 = the vmcnt field's maximum)
+                constexpr int V2 = 2 * ZDMA_PER_CHUNK < 63 ? 2 * ZDMA_PER_CHUNK : 63;
+                constexpr int V1 = ZDMA_PER_CHUNK < 63 ? ZDMA_PER_CHUNK : 63;
                 const int later = min(2, nch - 1 - q);
-                if (later >= 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-                else if (later == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                if (later >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(V2) : "memory");
+                else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(V1) : "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ZC_T(0)
             } else {
                 if (q + 1 < nch) stage(q + 1);                // loaded during the previous chunk
                 if (q + 2 < nch) load(q + 2);
@@ -194,7 +235,7 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                 if (cnt == ZC) {
                     // LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per
                     // sample; an LDS round trip per sample would set the pace instead)
-                    constexpr int ZB = 8;
+                    constexpr int ZB = OFS_ZC_ZB;
                     double2 xv[ZB / 2], ov[ZB / 2];
 #pragma unroll
                     for (int j = 0; j < ZB / 2; ++j) {
@@ -233,9 +274,36 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                     for (int u = 0; u < cnt; ++u) { acc = (acc + x[u]) - (ozero ? 0.0 : o[u]); r[u] = acc; }
                 }
             }
+            ZC_T(1)
         } else if (!OFS_ZC_NOHELP && q >= 1) {
             // ---- helpers: chunk q-1 (flags, stores, gate) ----
             const int qc = q - 1;
+            constexpr int NJ = (ZS + ZH - 1) / ZH;                 // streams per helper wave
+            // pass 1 (OFS_ZC_QUIET): the flags of every (row, stream) of this wave.  A chunk with no
+            // above sample and no open gate (the common case: events are sparse) needs no gate
+            // logic - its gate_mask rows are 0 - so the wave skips the scalar gate machine, whose
+            // dependent SALU / ballot chain per row dominated the helpers' time.
+            bool quiet = OFS_ZC_QUIET != 0;
+            double cv[ZR][NJ], lv[ZR][NJ];
+            uint64_t am[ZR][NJ];
+#pragma unroll
+            for (int rr = 0; rr < ZR; ++rr) {
+                const int64_t i = (int64_t)qc * ZC + 64 * rr + lane;
+                const bool vd = i < n && i >= a.W;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int s = (wv - 1) + ZH * j;
+                    const int sr = s < ns ? s : 0;
+                    cv[rr][j] = tc[qc % NC][sr][64 * rr + lane];
+                    lv[rr][j] = ta[qc & 1][sr][64 * rr + lane];
+                    const bool ab = s < ns && vd && (cv[rr][j] * a.scale >= lv[rr][j] * a.tv) && (cv[rr][j] >= a.minmag);
+                    am[rr][j] = __ballot(ab);
+                    if (am[rr][j]) quiet = false;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (g[j].open) quiet = false;
 #pragma unroll
             for (int rr = 0; rr < ZR; ++rr) {
             const int64_t base = (int64_t)qc * ZC + 64 * rr;
@@ -243,16 +311,27 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
             const bool inb = i < n;
             const bool vd = inb && i >= a.W;
 #pragma unroll
-            for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) {
+            for (int j = 0; j < NJ; ++j) {
                 const int s = (wv - 1) + ZH * j;
                 if (s >= ns) break;
-                ZGate& G = g[j];
-                const double c = tc[qc % NC][s][64 * rr + lane];
-                const double ls = ta[qc & 1][s][64 * rr + lane];
+                const double c = cv[rr][j];
+                const double ls = lv[rr][j];
                 const double cs = c * a.scale, th = ls * a.tv;
-                const bool ab = vd && (cs >= th) && (c >= a.minmag);
-                const uint64_t abm = __ballot(ab);
+                const uint64_t abm = am[rr][j];
+                const bool ab = (abm >> lane) & 1;
                 const int64_t o = (b0 + s) * n + i;
+                if (quiet) {
+                    if (inb) {
+                        if (a.local_sum) a.local_sum[o] = ls;
+                        if (a.corr_scaled) a.corr_scaled[o] = cs;
+                        if (a.thresh_scaled) a.thresh_scaled[o] = th;
+                        if (a.above) a.above[o] = 0;
+                        if (a.valid) a.valid[o] = (uint8_t)vd;
+                        if (a.gate_mask) a.gate_mask[o] = 0;
+                    }
+                    continue;
+                }
+                ZGate& G = g[j];
                 // gate in closed form (Hp >= 64): carried close first, then this row's first above
                 int close_l = -1;                                     // row lane of the close
                 if (G.open) {
@@ -304,8 +383,10 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
                 }
             }
             }
+            ZC_T(3)
         }
         lds_barrier();
+        if (wv == 0) { ZC_T(2) } else { ZC_T(4) }
     }
     // ---- gates still open at the end: gate_end = n, gate_mask[gate_start:n] ----
     if (wv >= 1) {
@@ -327,6 +408,10 @@ __global__ __launch_bounds__(64 * (1 + ZH)) void zc_cfar_kernel(ZcArgs a) {
             if (lane == 0 && a.n_ev) a.n_ev[b0 + s] = G.nev;
         }
     }
+#if OFS_ZC_TIMING
+    if (lane == 0)
+        for (int i = 0; i < 5; ++i) atomicAdd(&zc_prof[i], (unsigned long long)tacc[i]);
+#endif
 }
 
 }  // namespace
@@ -340,10 +425,23 @@ int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double 
     if (Hp < 64 || B <= 0 || n <= 0 || getenv("OFS_ZC_SEQ")) return 0;
     ZcArgs a{corr_mag, B, n, W, tv, scale, minmag, reflen, Hp, local_sum, corr_scaled, thresh_scaled,
              above, valid, gate_mask, max_ev, n_ev, ev, ev_v};
-    const int64_t grid = (B + ZS - 1) / ZS;
+    constexpr int SD = OFS_ZC_S, HD = OFS_ZC_H, SR = OFS_ZC_S_REG, HR = OFS_ZC_H_REG;
     const bool dma = ZC % 128 == 0 && n % ZC == 0 && W % ZC == 0 && W >= 0 &&
                      (reinterpret_cast<uintptr_t>(corr_mag) & 15) == 0 && !getenv("OFS_ZC_NODMA");
-    if (dma) hipLaunchKernelGGL(zc_cfar_kernel<true>, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
-    else hipLaunchKernelGGL(zc_cfar_kernel<false>, dim3((unsigned)grid), dim3(64 * (1 + ZH)), 0, st, a);
+    if (dma) hipLaunchKernelGGL((zc_cfar_kernel<true, SD, HD>), dim3((unsigned)((B + SD - 1) / SD)), dim3(64 * (1 + HD)), 0, st, a);
+    else hipLaunchKernelGGL((zc_cfar_kernel<false, SR, HR>), dim3((unsigned)((B + SR - 1) / SR)), dim3(64 * (1 + HR)), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
+
+#if OFS_ZC_TIMING
+// per-role cycle totals of zc_cfar_kernel since the last call (diagnostic builds): walker DMA wait,
+// walker chain, walker barrier, helper work, helper barrier
+extern "C" int ofs_zc_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(zc_prof), 5 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(zc_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+extern "C" int ofs_zc_hwid(unsigned* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(zc_hwid), 4096 * 8 * sizeof(unsigned)) == hipSuccess ? 0 : -1;
+}
+#endif

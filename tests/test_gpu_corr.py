@@ -187,11 +187,13 @@ def test_zc_detect_preamble_vs_reference_golden():
 
 
 @pytest.mark.parametrize("hyst,B,n,W", [(0, 4, 3000, 128), (1, 4, 3000, 128), (5, 4, 3000, 128), (64, 4, 3000, 128),
-                                         (64, 11, 4096, 256), (100, 9, 2048, 128), (64, 5, 1536, 512)])
+                                         (64, 11, 4096, 256), (100, 9, 2048, 128), (64, 5, 1536, 512),
+                                         (256, 37, 2048, 256), (256, 20, 4096, 1024)])
 def test_zc_cfar_and_gate_bit_identical_given_corr_mag(hyst, B, n, W):
     """CFAR + gate vs the oracle, bit for bit: the sequential kernel (hysteresis < 64), the fused
     lane-per-stream kernel with register-staged tiles (n not a whole number of chunks) and with
-    LDS-DMA tiles (n and W whole chunks; 11 and 9 streams leave a workgroup's rows unused)."""
+    LDS-DMA tiles (n and W whole chunks; 11, 9, 37 and 20 streams leave a workgroup's rows unused;
+    37 and 20 span several 16-stream DMA-path workgroups; hysteresis 256 is zc_v2's own)."""
     rng = np.random.default_rng(hyst + n)
     mag = np.abs(rng_c(rng, B, n)) * 0.2
     for b in range(B):
