@@ -699,6 +699,10 @@ int zs_bpl(int n_br) {
 
 bool zs_plan(int n_br, int N, int bpl, int& C, int& W, size_t& lds, int64_t noff) {
     C = (N >= 8192 && N % 256 == 0) ? 256 : (N % 128 == 0 ? 128 : 64);
+    if (const char* e = getenv("OFS_ZS_C")) {                         // A/B: chunk length override
+        const int c = atoi(e);
+        if (c >= 64 && c <= 256 && c % 64 == 0 && N % c == 0) C = c;
+    }
     const int64_t nchunks = (noff + C - 1) / C;
     W = (int)std::min<int64_t>(n_br == 1 ? 16 : 8, (nchunks + bpl - 1) / bpl);
     const int stg = zs_stg(C, bpl);
