@@ -99,6 +99,12 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_ZB
 #define OFS_ZC_ZB 8                // walker: samples per LDS batch (read one batch ahead of the adds)
 #endif
+#ifndef OFS_ZC_DIAG_NOLDS
+#define OFS_ZC_DIAG_NOLDS 0        // diagnostic builds (timing only, wrong results): helpers read no LDS
+#endif
+#ifndef OFS_ZC_DIAG_NOST
+#define OFS_ZC_DIAG_NOST 0         // ... helpers store nothing on quiet chunks
+#endif
 #ifndef OFS_ZC_QUIET
 #define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
 #endif
@@ -118,9 +124,10 @@ void zc_cfar_kernel(ZcArgs a) {
     __shared__ double to[NO][ZS][ZP];     // c[i - W] (0 before the window fills)
     __shared__ double ta[2][ZS][ZP];      // running sum after sample i
     const int lane = threadIdx.x & 63;
-    // role of this wave: 0 = walker, 1..ZH = helpers.  (Choosing the walker by SIMD id, so that
-    // both workgroups of a CU put their walkers on one SIMD, measured slower: 0.38 -> 0.45 ms.)
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // role of this wave: 0 = walker, 1..ZH = helpers.  (Measured and not kept: the walker chosen by
+    // SIMD id so both workgroups' walkers share a SIMD, 0.38 -> 0.45 ms; an idle 8th wave as the
+    // walker's SIMD partner, 0.362 -> 0.373 ms: SIMD sharing is not what slows the chain.)
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int64_t b0 = (int64_t)blockIdx.x * ZS;
     const int ns = (int)min((int64_t)ZS, a.B - b0);          // streams of this workgroup
     const int64_t n = a.n;
@@ -281,22 +288,33 @@ void zc_cfar_kernel(ZcArgs a) {
             constexpr int NJ = (ZS + ZH - 1) / ZH;                 // streams per helper wave
             // pass 1 (OFS_ZC_QUIET): the flags of every (row, stream) of this wave.  A chunk with no
             // above sample and no open gate (the common case: events are sparse) needs no gate
-            // logic - its gate_mask rows are 0 - so the wave skips the scalar gate machine, whose
-            // dependent SALU / ballot chain per row dominated the helpers' time.
+            // logic - its gate_mask rows are 0 - so the wave skips the scalar gate machine.
             bool quiet = OFS_ZC_QUIET != 0;
             double cv[ZR][NJ], lv[ZR][NJ];
             uint64_t am[ZR][NJ];
+            // every LDS read of the chunk first (one latency for all of them, not one per row),
+            // then the flags with non-short-circuit logic (no exec-mask branches per term)
 #pragma unroll
-            for (int rr = 0; rr < ZR; ++rr) {
-                const int64_t i = (int64_t)qc * ZC + 64 * rr + lane;
-                const bool vd = i < n && i >= a.W;
+            for (int rr = 0; rr < ZR; ++rr)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
                     const int s = (wv - 1) + ZH * j;
                     const int sr = s < ns ? s : 0;
+#if OFS_ZC_DIAG_NOLDS                                           // diagnostic: no helper LDS reads
+                    cv[rr][j] = 1e-3 * (double)(lane + sr) + (double)qc; lv[rr][j] = cv[rr][j] * 1e30;
+#else
                     cv[rr][j] = tc[qc % NC][sr][64 * rr + lane];
                     lv[rr][j] = ta[qc & 1][sr][64 * rr + lane];
-                    const bool ab = s < ns && vd && (cv[rr][j] * a.scale >= lv[rr][j] * a.tv) && (cv[rr][j] >= a.minmag);
+#endif
+                }
+#pragma unroll
+            for (int rr = 0; rr < ZR; ++rr) {
+                const int64_t i = (int64_t)qc * ZC + 64 * rr + lane;
+                const bool vd = (i < n) & (i >= a.W);
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int s = (wv - 1) + ZH * j;
+                    const bool ab = (s < ns) & vd & (cv[rr][j] * a.scale >= lv[rr][j] * a.tv) & (cv[rr][j] >= a.minmag);
                     am[rr][j] = __ballot(ab);
                     if (am[rr][j]) quiet = false;
                 }
@@ -321,7 +339,7 @@ void zc_cfar_kernel(ZcArgs a) {
                 const bool ab = (abm >> lane) & 1;
                 const int64_t o = (b0 + s) * n + i;
                 if (quiet) {
-                    if (inb) {
+                    if (inb && !OFS_ZC_DIAG_NOST) {
                         if (a.local_sum) a.local_sum[o] = ls;
                         if (a.corr_scaled) a.corr_scaled[o] = cs;
                         if (a.thresh_scaled) a.thresh_scaled[o] = th;
