@@ -105,6 +105,12 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_DIAG_NOST
 #define OFS_ZC_DIAG_NOST 0         // ... helpers store nothing on quiet chunks
 #endif
+#ifndef OFS_ZC_WUNROLL
+#define OFS_ZC_WUNROLL 16          // walker: LDS batches unrolled per chunk (code size A/B)
+#endif
+#ifndef OFS_ZC_HUNROLL
+#define OFS_ZC_HUNROLL 2           // helpers: rows of the gate pass unrolled (code size A/B)
+#endif
 #ifndef OFS_ZC_QUIET
 #define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
 #endif
@@ -250,7 +256,7 @@ void zc_cfar_kernel(ZcArgs a) {
                         ov[j] = reinterpret_cast<const double2*>(o)[j];
                         if (ozero) ov[j] = make_double2(0.0, 0.0);
                     }
-#pragma unroll
+#pragma unroll OFS_ZC_WUNROLL
                     for (int bb = 0; bb < ZC / ZB; ++bb) {
                         double2 xn[ZB / 2], on[ZB / 2];
                         if (bb + 1 < ZC / ZB) {
@@ -322,7 +328,7 @@ void zc_cfar_kernel(ZcArgs a) {
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
                 if (g[j].open) quiet = false;
-#pragma unroll
+#pragma unroll OFS_ZC_HUNROLL
             for (int rr = 0; rr < ZR; ++rr) {
             const int64_t base = (int64_t)qc * ZC + 64 * rr;
             const int64_t i = base + lane;
