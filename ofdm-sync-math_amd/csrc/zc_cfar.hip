@@ -114,6 +114,52 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_QUIET
 #define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
 #endif
+// walker: the exact left-to-right recursion of RunningSum.step over one full chunk of this lane's
+// stream; LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per sample; an
+// LDS round trip per sample would set the pace instead).  OZ: c[i-W] is 0 (window not yet full).
+template <int ZCN, bool OZ>
+__device__ __forceinline__ void zc_walk_chunk(const double* x, const double* o, double* r, double& acc) {
+#pragma clang fp contract(off)
+    constexpr int ZB = OFS_ZC_ZB;
+    double2 xv[ZB / 2], ov[ZB / 2];
+#pragma unroll
+    for (int j = 0; j < ZB / 2; ++j) {
+        xv[j] = reinterpret_cast<const double2*>(x)[j];
+        if (!OZ) ov[j] = reinterpret_cast<const double2*>(o)[j];
+    }
+#pragma unroll OFS_ZC_WUNROLL
+    for (int bb = 0; bb < ZCN / ZB; ++bb) {
+        double2 xn[ZB / 2], on[ZB / 2];
+        if (bb + 1 < ZCN / ZB) {
+#pragma unroll
+            for (int j = 0; j < ZB / 2; ++j) {
+                xn[j] = reinterpret_cast<const double2*>(x + (bb + 1) * ZB)[j];
+                if (!OZ) on[j] = reinterpret_cast<const double2*>(o + (bb + 1) * ZB)[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ZB / 2; ++j) {
+            double2 rr;
+#if OFS_ZC_NOCHAIN
+            rr.x = xv[j].x - (OZ ? 0.0 : ov[j].x); rr.y = xv[j].y - (OZ ? 0.0 : ov[j].y);
+#else
+            if (OZ) {
+                acc = acc + xv[j].x; rr.x = acc;
+                acc = acc + xv[j].y; rr.y = acc;
+            } else {
+                acc = (acc + xv[j].x) - ov[j].x; rr.x = acc;
+                acc = (acc + xv[j].y) - ov[j].y; rr.y = acc;
+            }
+#endif
+            reinterpret_cast<double2*>(r + bb * ZB)[j] = rr;
+        }
+        if (bb + 1 < ZCN / ZB) {
+#pragma unroll
+            for (int j = 0; j < ZB / 2; ++j) { xv[j] = xn[j]; if (!OZ) ov[j] = on[j]; }
+        }
+    }
+}
+
 template <bool DMA, int ZS, int ZH>
 __global__ __launch_bounds__(64 * (1 + ZH))
 void zc_cfar_kernel(ZcArgs a) {
@@ -246,43 +292,10 @@ void zc_cfar_kernel(ZcArgs a) {
                 const bool ozero = DMA && (int64_t)q * ZC < a.W;      // DMA path: before the window fills
                 double* r = ta[q & 1][lane];
                 if (cnt == ZC) {
-                    // LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per
-                    // sample; an LDS round trip per sample would set the pace instead)
-                    constexpr int ZB = OFS_ZC_ZB;
-                    double2 xv[ZB / 2], ov[ZB / 2];
-#pragma unroll
-                    for (int j = 0; j < ZB / 2; ++j) {
-                        xv[j] = reinterpret_cast<const double2*>(x)[j];
-                        ov[j] = reinterpret_cast<const double2*>(o)[j];
-                        if (ozero) ov[j] = make_double2(0.0, 0.0);
-                    }
-#pragma unroll OFS_ZC_WUNROLL
-                    for (int bb = 0; bb < ZC / ZB; ++bb) {
-                        double2 xn[ZB / 2], on[ZB / 2];
-                        if (bb + 1 < ZC / ZB) {
-#pragma unroll
-                            for (int j = 0; j < ZB / 2; ++j) {
-                                xn[j] = reinterpret_cast<const double2*>(x + (bb + 1) * ZB)[j];
-                                on[j] = reinterpret_cast<const double2*>(o + (bb + 1) * ZB)[j];
-                                if (ozero) on[j] = make_double2(0.0, 0.0);
-                            }
-                        }
-#pragma unroll
-                        for (int j = 0; j < ZB / 2; ++j) {
-                            double2 rr;
-#if OFS_ZC_NOCHAIN
-                            rr.x = xv[j].x - ov[j].x; rr.y = xv[j].y - ov[j].y;
-#else
-                            acc = (acc + xv[j].x) - ov[j].x; rr.x = acc;
-                            acc = (acc + xv[j].y) - ov[j].y; rr.y = acc;
-#endif
-                            reinterpret_cast<double2*>(r + bb * ZB)[j] = rr;
-                        }
-                        if (bb + 1 < ZC / ZB) {
-#pragma unroll
-                            for (int j = 0; j < ZB / 2; ++j) { xv[j] = xn[j]; ov[j] = on[j]; }
-                        }
-                    }
+                    // ozero is uniform per chunk: a chain without the c[i-W] reads and selects
+                    // (x - 0.0 == x exactly, -0.0 included) instead of two v_cndmask per sample
+                    if (ozero) zc_walk_chunk<ZC, true>(x, o, r, acc);
+                    else zc_walk_chunk<ZC, false>(x, o, r, acc);
                 } else {
                     for (int u = 0; u < cnt; ++u) { acc = (acc + x[u]) - (ozero ? 0.0 : o[u]); r[u] = acc; }
                 }
