@@ -90,24 +90,29 @@ class ZCDetectionResult:
     state: ZCDetectionState
 
 
-def _ref_key(reference) -> tuple:
-    """Cheap identity of a reference for the plan cache, without a device-to-host copy: the
-    content digest of a host array, or (pointer, version counter, size) of a device tensor."""
+def _ref_host(reference) -> np.ndarray:
+    """The reference taps as a contiguous complex128 host array (a device tensor is copied: a
+    few KB, once per call).  Everything that identifies a reference - the plan-cache key, the
+    energy - is computed from these bytes, never from a device address: the caching allocator
+    hands a freed reference's address to the next one, so (data_ptr, _version) does not
+    identify contents."""
     if isinstance(reference, torch.Tensor):
-        return ("dev", reference.data_ptr(), reference._version, reference.numel(), str(reference.dtype))
+        return np.ascontiguousarray(reference.detach().to(torch.complex128).cpu().numpy().reshape(-1))
+    return np.ascontiguousarray(np.asarray(reference, dtype=np.complex128).reshape(-1))
+
+
+def _ref_key(r_host: np.ndarray) -> tuple:
+    """Content identity of a reference for the plan cache: digest of its complex128 bytes."""
     import hashlib
-    r = np.ascontiguousarray(np.asarray(reference, dtype=np.complex128))
-    return ("host", hashlib.sha1(r.tobytes()).hexdigest(), r.size)
+    return (hashlib.sha1(r_host.tobytes()).hexdigest(), r_host.size)
 
 
-def _ref_dev(reference, dev):
-    r = reference
-    if isinstance(r, torch.Tensor):
-        energy = float(torch.sum(torch.abs(r.to(torch.complex128)) ** 2))
-        return r.to(device=dev, dtype=torch.complex128).contiguous(), energy
-    r = np.asarray(r, dtype=np.complex128)
-    energy = float(np.sum(np.abs(r) ** 2))          # as the reference computes it (zc_v2.py:263)
-    return torch.from_numpy(np.ascontiguousarray(r)).to(dev), energy
+def _ref_dev(reference, r_host: np.ndarray, dev):
+    """(device complex128 taps, energy); energy as the reference computes it (zc_v2.py:263)."""
+    energy = float(np.sum(np.abs(r_host) ** 2))
+    if isinstance(reference, torch.Tensor):
+        return reference.to(device=dev, dtype=torch.complex128).contiguous().reshape(-1), energy
+    return torch.from_numpy(r_host).to(dev), energy
 
 
 class MFPlan:
@@ -121,8 +126,7 @@ class MFPlan:
     def __init__(self, reference, B: int, nb: int, T: int, dev, M: int = 0):
         import ctypes
         import threading
-        r = np.ascontiguousarray(np.asarray(reference.cpu().numpy() if isinstance(reference, torch.Tensor)
-                                            else reference, dtype=np.complex128))
+        r = _ref_host(reference)
         self._lib = _lib.lib()
         h, wb, sb = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_size_t()
         _lib.check(self._lib.ofs_zc_mf_plan_create(r.ctypes.data, r.size, int(B), int(nb), int(T), int(M),
@@ -183,7 +187,8 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     cannot hold (ofs_zc_mf_plan_create -> OFS_ETOOLONG: e.g. 4 branches at N = 2048)."""
     batch = _lib.as_batch(x, batched=True)
     dev = batch.data.device
-    ref, energy = _ref_dev(reference, dev)
+    r_host = _ref_host(reference)
+    ref, energy = _ref_dev(reference, r_host, dev)
     N = int(ref.numel())
     nout = batch.T + N - 1
     shape = (batch.B, batch.nb, nout) if mode == OFS_ZC_RAW else (batch.B, nout)
@@ -194,7 +199,7 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     use_fft = mode != OFS_ZC_NORMALIZE and batch.B > 0 and batch.T > 0 and (
         method == "fft" or (method == "auto" and N >= FFT_MIN_TAPS))
     if use_fft:
-        plan = _mf_plan(reference, _ref_key(reference), batch.B, batch.nb, batch.T, dev)
+        plan = _mf_plan(r_host, _ref_key(r_host), batch.B, batch.nb, batch.T, dev)
         if plan is not None:
             plan.run(batch, energy, mode, corr, mag)
             return corr, mag

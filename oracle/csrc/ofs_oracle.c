@@ -437,9 +437,14 @@ static inline double fp32_metric_bound(double c, double R, double M, double bP, 
  * S&C) and Mm, Pm, Rm (Minn), fp32.  stats [B][8]:
  *   0 max|ΔMc|   1 max |ΔMc|/bound   2 max |ΔPc|/boundP   3 max |ΔRc|/boundR
  *   4 max |ΔMm|/max(1, Mm)   5 max |ΔMm|/bound   6 max |ΔPm|/boundP   7 max |ΔRm|/boundR */
+static inline double out_at(const void* a, int out_f64, int64_t i) {
+    return out_f64 ? ((const double*)a)[i] : (double)((const float*)a)[i];
+}
+
 int oracle_sc_minn_check(const void* x, int is_c128, int64_t B, int64_t nb, int64_t T, int64_t N,
-                         const float* Mc, const float* Pc, const float* Rc, const float* Mm, const float* Pm,
-                         const float* Rm, double kP, double kR, double kM, double* stats, int nthreads) {
+                         const void* Mc, const void* Pc, const void* Rc, const void* Mm, const void* Pm,
+                         const void* Rm, int out_f64, double kP, double kR, double kM, double* stats,
+                         int nthreads) {
     if (!x || B < 0 || nb < 1 || N < 4 || N % 4 || T < N || !Mc || !Pc || !Rc || !Mm || !Pm || !Rm || !stats)
         return -1;
 #ifdef _OPENMP
@@ -471,8 +476,8 @@ int oracle_sc_minn_check(const void* x, int is_c128, int64_t B, int64_t nb, int6
                     const double pr = o[d], pi = o[nout + d], R = o[2 * nout + d], S = o[3 * nout + d];
                     const double ap = hypot(pr, pi), Rm_ = R > 1e-12 ? R : 1e-12, M = ap * ap / (Rm_ * Rm_);
                     const double bP = kP * u * S + u * ap, bR = kR * u * R;
-                    const double dP = hypot((double)Pc[2 * g] - pr, (double)Pc[2 * g + 1] - pi);
-                    const double dR = fabs((double)Rc[g] - R), dM = fabs((double)Mc[g] - M);
+                    const double dP = hypot(out_at(Pc, out_f64, 2 * g) - pr, out_at(Pc, out_f64, 2 * g + 1) - pi);
+                    const double dR = fabs(out_at(Rc, out_f64, g) - R), dM = fabs(out_at(Mc, out_f64, g) - M);
                     const double bM = fp32_metric_bound(ap, R, M, bP, bR, kM);
                     if (!(dM <= st[0])) st[0] = dM;                     /* NaN propagates as a failure */
                     if (!(dM / bM <= st[1])) st[1] = dM / bM;
@@ -484,8 +489,8 @@ int oracle_sc_minn_check(const void* x, int is_c128, int64_t B, int64_t nb, int6
                     const double pr = o[4 * nout + d], pi = o[5 * nout + d], R = o[6 * nout + d], S = o[7 * nout + d];
                     const double c = pr > 0.0 ? pr : 0.0, Rm_ = R > 1e-12 ? R : 1e-12, M = c * c / (Rm_ * Rm_);
                     const double bP = kP * u * S + u * hypot(pr, pi), bR = kR * u * R;
-                    const double dP = hypot((double)Pm[2 * g] - pr, (double)Pm[2 * g + 1] - pi);
-                    const double dR = fabs((double)Rm[g] - R), dM = fabs((double)Mm[g] - M);
+                    const double dP = hypot(out_at(Pm, out_f64, 2 * g) - pr, out_at(Pm, out_f64, 2 * g + 1) - pi);
+                    const double dR = fabs(out_at(Rm, out_f64, g) - R), dM = fabs(out_at(Mm, out_f64, g) - M);
                     const double bM = fp32_metric_bound(c, R, M, bP, bR, kM);
                     const double rn = dM / (M > 1.0 ? M : 1.0);
                     if (!(rn <= st[4])) st[4] = rn;

@@ -31,7 +31,7 @@ def lib():
         l.oracle_max_threads.restype = c_int
         l.oracle_sc_minn_check.restype = c_int
         l.oracle_sc_minn_check.argtypes = [c_void_p, c_int, c_int64, c_int64, c_int64, c_int64] + [c_void_p] * 6 + \
-            [c_double, c_double, c_double, c_void_p, c_int]
+            [c_int, c_double, c_double, c_double, c_void_p, c_int]
         l.oracle_zc_freq_check.restype = c_int
         l.oracle_zc_freq_check.argtypes = [c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
                                            c_void_p, c_void_p, c_double, c_void_p, c_int, c_double, c_double,
@@ -110,20 +110,27 @@ SC_MINN_STATS = ("comb_max_dM", "comb_dM_over_bound", "comb_dP_over_bound", "com
 
 
 def sc_minn_check(x, N, Mc, Pc, Rc, Mm, Pm, Rm, kP, kR, kM, nthreads=0):
-    """Engine fp32 combined S&C + Minn outputs ([B, T-N+1]) against the fp64 reference values of
-    x [B, nb, T] (oracle_sc_minn_check).  Returns the per-stream statistics [B, 8] (SC_MINN_STATS)."""
+    """Engine combined S&C + Minn outputs ([B, T-N+1]; fp32 / complex64, or fp64 / complex128 for
+    all six) against the fp64 reference values of x [B, nb, T] (oracle_sc_minn_check).  Returns the
+    per-stream statistics [B, 8] (SC_MINN_STATS)."""
     x = np.ascontiguousarray(x)
     if x.ndim == 2:
         x = x[:, None, :]
     if x.dtype not in (np.complex64, np.complex128):
         raise TypeError("x must be complex64 / complex128")
     B, nb, T = x.shape
-    f32 = [_host(a, np.float32) for a in (Mc, Rc, Mm, Rm)]
-    c64 = [_host(a, np.complex64) for a in (Pc, Pm)]
+    f64 = np.asarray(Mc).dtype == np.float64
+    rt, ct = (np.float64, np.complex128) if f64 else (np.float32, np.complex64)
+    fr = [_host(a, rt) for a in (Mc, Rc, Mm, Rm)]
+    cp = [_host(a, ct) for a in (Pc, Pm)]
+    nout = T - int(N) + 1
+    for a in fr + cp:
+        if a.size != B * nout:
+            raise ValueError(f"outputs must be [B, T-N+1] = [{B}, {nout}]")
     st = np.zeros((B, 8))
     rc = lib().oracle_sc_minn_check(x.ctypes.data, int(x.dtype == np.complex128), B, nb, T, int(N),
-                                    f32[0].ctypes.data, c64[0].ctypes.data, f32[1].ctypes.data, f32[2].ctypes.data,
-                                    c64[1].ctypes.data, f32[3].ctypes.data, float(kP), float(kR), float(kM),
+                                    fr[0].ctypes.data, cp[0].ctypes.data, fr[1].ctypes.data, fr[2].ctypes.data,
+                                    cp[1].ctypes.data, fr[3].ctypes.data, int(f64), float(kP), float(kR), float(kM),
                                     st.ctypes.data, int(nthreads))
     if rc:
         raise RuntimeError(f"oracle_sc_minn_check failed ({rc})")

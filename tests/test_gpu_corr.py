@@ -483,6 +483,31 @@ def test_zc_detect_four_branches_n2048_falls_back_to_direct():
     assert k >= 1 and np.min(np.abs(r.events[0, :k, 0].cpu().numpy() - (1500 + 2047))) <= 2
 
 
+def test_zc_fft_plan_cache_device_references_at_recycled_address():
+    """Two different same-length device references allocated back to back, the first freed before
+    the second exists, so torch's caching allocator gives the second the first's address (and the
+    same version counter 0): the plan cache keys by content, so each call correlates with its own
+    reference and equals the oracle (a key on data_ptr/_version returned the first plan's spectrum)."""
+    rng = np.random.default_rng(46)
+    x = rng_c(rng, 2, 1, 9000)
+    xd = torch.from_numpy(x).cuda()
+    ptrs = []
+    for root in (25, 29, 34):
+        ref_h = O.pss_symbol(2048, root=root)
+        x_r = x.copy()
+        x_r[0, 0, 3000:3000 + ref_h.size] += ref_h
+        xd.copy_(torch.from_numpy(x_r))
+        ref_d = torch.as_tensor(ref_h, device="cuda")
+        ptrs.append(ref_d.data_ptr())
+        _, mag = zc_v2.correlate_batched(xd, ref_d, zc_v2.OFS_ZC_V2, want_corr=False, want_mag=True, method="fft")
+        mag = mag.cpu().numpy()
+        del ref_d
+        for b in range(2):
+            want = np.abs(O.normalize_correlation(O.matched_filter(x_r[b, 0], ref_h), x_r[b, 0], ref_h))
+            np.testing.assert_allclose(mag[b], want, rtol=1e-9, atol=1e-12)
+    assert len(set(ptrs)) < len(ptrs), "the allocator did not recycle the address; the test is vacuous"
+
+
 def test_zc_fft_plan_shared_by_two_streams():
     """One cached overlap-save plan used from two HIP streams back to back: each call takes its own
     scratch / work buffers from torch's stream-ordered allocator, so the results equal the
