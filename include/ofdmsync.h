@@ -66,6 +66,45 @@ const char* ofs_source_hash(void);
 const char* ofs_status_string(int32_t status);
 
 /*
+ * Debug / A-B variants (not part of the reference interface; no reference counterpart).
+ * Every dispatch decision and every arithmetic choice of the library depends only on the call's
+ * arguments, EXCEPT where a variant has been set through this one entry point.  Variants exist
+ * so the tests can force an alternative kernel on the same input (e.g. the general LDS engine
+ * against the integer-exact wave kernel, the rocFFT matched-filter pipeline against the fused LDS
+ * FFT) and the measurement tools can time both.  Nothing reads the environment.  All variants
+ * start unset (OFS_VARIANT_UNSET); a process that never calls ofs_debug_set_variant runs the
+ * default dispatch.  Names (value meaning):
+ *   EXACT        0: sync_aa / minn_rtl integer-exact and fp64 wave kernels off (general engine)
+ *   FAST_E       2|4|8: samples per lane of the storing aa_fast kernel
+ *   FAST_E_DO    2|4|8: samples per lane of the detect-only aa_fast kernel
+ *   FAST_SCAN    32|64: row-scan precision of the storing aa_fast kernel (default 64)
+ *   FAST_SCAN_DO 32|64: row-scan precision of the detect-only aa_fast kernel (default 32)
+ *   RTL_WPB      1|2: streams per workgroup of rtl_exact_kernel (default 4)
+ *   PARK_DIRECT  1: Park energies as direct window sums (no shared-window split)
+ *   ZW64         0: zc_freq N = 4096 window FFT through zc_win_kernel instead of zc_win64_kernel
+ *   ZW64_GRID    n > 0: cap of the persistent zc_win64 grid (default: CU count)
+ *   ZS           0: zc_freq fp64 through the round-2 one-chunk-per-wave kernel
+ *   ZF_ITEMS     n > 0: chunk-count target of that kernel (default 4096)
+ *   ZS_PAIR      0: per-bin sliding DFT instead of the pair resonators
+ *   ZS_DEFER     0|1: row sums per step (DPP) / deferred through LDS
+ *   ZS_BPL       4: bins per lane of the one-branch sliding kernel (default 8)
+ *   ZS_C         64|128|192|256: chunk length of the sliding kernels (must divide N)
+ *   ZS_GBLK      0: Horner block DFTs in the pair kernel instead of Goertzel
+ *   MC_FUSED     0: ZC matched filter through the rocFFT pipeline instead of the fused LDS FFT
+ *   MC_FUSE_X    0: fused LDS FFT with the separate extract kernel
+ *   ZC_SEQ       1: zc_v2 CFAR + gate through the sequential one-wave-per-stream kernel
+ *   ZC_NODMA     1: zc_v2 CFAR tiles through registers instead of LDS-DMA
+ *   BE_FAST      0: receiver back-end through the generic kernel
+ * ofs_debug_set_variant returns OFS_EINVAL for an unknown name; value OFS_VARIANT_UNSET clears
+ * one variant, ofs_debug_reset_variants clears all.  Not for concurrent use with running calls
+ * (a call reads each variant once, at dispatch).
+ */
+#define OFS_VARIANT_UNSET INT64_MIN
+int32_t ofs_debug_set_variant(const char* name, int64_t value);
+int64_t ofs_debug_get_variant(const char* name);
+int32_t ofs_debug_reset_variants(void);
+
+/*
  * [A][A] streaming Schmidl-Cox detector.
  * Replaces sync_aa.aa_detect_streaming (sync_aa.py:421-571): P[n], R[n], M[n], valid[n]
  * (sync_aa.py:458-493) and, if detect != 0, the gate/peak/CFO events (sync_aa.py:495-568).

@@ -701,9 +701,8 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 }
 
 // ---- dispatch -------------------------------------------------------------------------------
-bool exact_enabled() {                  // OFS_EXACT=0 forces the general engine (A/B, tests)
-    const char* s = getenv("OFS_EXACT");
-    return !(s && s[0] == '0');
+bool exact_enabled() {                  // variant EXACT=0 forces the general engine (A/B, tests)
+    return !ofs::variant_off(ofs::V_EXACT);
 }
 
 template <int E, int MR, int NA>
@@ -739,8 +738,8 @@ template <int E, int MW, int CPNA, int NBM>
 int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
     const size_t per_wave = rtl_wave_lds(E, MW, a.nb);
     int wpb = 4;                                             // waves (streams) per workgroup
-    const char* ev = getenv("OFS_RTL_WPB");                  // tuning: 1, 2 or 4
-    if (ev && (atoi(ev) == 1 || atoi(ev) == 2)) wpb = atoi(ev);
+    const int64_t wv = ofs::variant(ofs::V_RTL_WPB);        // tuning: 1, 2 or 4
+    if (wv == 1 || wv == 2) wpb = (int)wv;
     while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
     const size_t lds = per_wave * wpb;
     auto k = rtl_exact_kernel<E, MW, CPNA, NBM>;

@@ -559,12 +559,12 @@ int launch_stream_mr(int mr, const AaFastArgs& a, hipStream_t st) {
     return 0;
 }
 
-// row-scan precision of the register-staged kernel, read per call: the detect-only launch scans
-// in fp32 unless OFS_FAST_SCAN_DO=64, the storing launch in fp64 unless OFS_FAST_SCAN=32 (tests
-// run the storing kernel with the detect-only arithmetic to classify its events, A/B)
+// row-scan precision of the register-staged kernel: the detect-only launch scans in fp32, the
+// storing launch in fp64; variants FAST_SCAN_DO / FAST_SCAN = 32 | 64 override (tests run the
+// storing kernel with the detect-only arithmetic to classify its events, A/B)
 bool scan32(bool det_only) {
-    const char* s = getenv(det_only ? "OFS_FAST_SCAN_DO" : "OFS_FAST_SCAN");
-    if (s && (s[0] == '3' || s[0] == '6')) return s[0] == '3';
+    const int64_t v = ofs::variant(det_only ? ofs::V_FAST_SCAN_DO : ofs::V_FAST_SCAN);
+    if (v == 32 || v == 64) return v == 32;
     return det_only;
 }
 
@@ -601,9 +601,8 @@ int launch_e(int E, int mr, const AaFastArgs& a, hipStream_t st) {
 }
 
 int pick_e(int L) {
-    // samples per lane per row; override for tuning with OFS_FAST_E=2|4|8 (read per call)
-    const char* s = getenv("OFS_FAST_E");
-    const int forced = s ? atoi(s) : 0;
+    // samples per lane per row; variant FAST_E = 2|4|8 overrides (A/B, parity classification)
+    const int forced = (int)ofs::variant_or(ofs::V_FAST_E, 0);
     if (forced == 2 || forced == 4 || forced == 8) return (L % (64 * forced) == 0) ? forced : 0;
     for (int e : {2, 4, 8})                                  // E=2 measured 3 % faster than 4 (r01c)
         if (L % (64 * e) == 0) return e;
@@ -613,10 +612,9 @@ int pick_e(int L) {
 // detect-only (events without P/R/M stores: VALU/issue-bound, not HBM-bound, SQ counters r03a):
 // samples per lane per row.  With fp32 row scans (3 x ~7 VALU per row instead of ~25) E = 4 is
 // the fastest (r03f: 0.1071 ms vs 0.1134 at E = 8, 0.1191 / 0.1193 with fp64 scans at E = 4 / 8);
-// override with OFS_FAST_E_DO=2|4|8.
+// variant FAST_E_DO = 2|4|8 overrides.
 int pick_e_do(int L) {
-    const char* s = getenv("OFS_FAST_E_DO");
-    const int forced = s ? atoi(s) : 0;
+    const int forced = (int)ofs::variant_or(ofs::V_FAST_E_DO, 0);
     for (int e : {forced, 4, 8, 2})
         if ((e == 2 || e == 4 || e == 8) && L % (64 * e) == 0) return e;
     return 0;

@@ -340,7 +340,7 @@ __device__ __forceinline__ void place_window(const BeArgs& a, int64_t s, double 
 //    go to LDS;
 //  * the twiddle table holds N/4 entries (w^{j+N/4} = -i·w^j);
 // so a workgroup needs N·16 + N/4·16 + n_used·8 bytes of LDS (50 KB at N = 2048): 3 per CU.
-// OFS_BE_FAST=0 selects the generic kernel (A/B).
+// variant BE_FAST=0 selects the generic kernel (A/B).
 #ifndef OFS_BE_TIMING
 #define OFS_BE_TIMING 0            // diagnostic builds: per-phase cycles (tools/be_phase.py)
 #endif
@@ -873,8 +873,7 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BW), lds, st, a);
         return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
     };
-    const char* fe = getenv("OFS_BE_FAST");                 // 0: the generic kernel (A/B)
-    const bool fast = !(fe && atoi(fe) == 0) && (n_br == 1 || n_br == 2) && cp_len <= 2 * BW &&
+    const bool fast = !ofs::variant_off(ofs::V_BE_FAST) &&    // variant BE_FAST=0: the generic kernel (A/B) (n_br == 1 || n_br == 2) && cp_len <= 2 * BW &&
                       ((n_fft == 4 * BW && n_used <= 3 * BW) || (n_fft == 8 * BW && n_used <= 5 * BW) ||
                        (n_fft == 16 * BW && n_used <= 10 * BW));
     if (fast) {

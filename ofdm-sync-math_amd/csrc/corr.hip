@@ -944,8 +944,8 @@ static int park_launch(const void* x, int64_t B, int nb, int64_t T, int half, in
                        void* M, void* P, void* E, hipStream_t st) {
     const int64_t len = CD + 2 * (int64_t)half - 2 + 2 * PADF;
     const size_t lds = (size_t)split_stride(len) * OPT * sizeof(typename C2<R>::T);
-    // shared-window energy needs half >= OPT - 1 (OFS_PARK_DIRECT=1: per-output energy sums, A/B)
-    static const bool direct = getenv("OFS_PARK_DIRECT") != nullptr;
+    // shared-window energy needs half >= OPT - 1 (variant PARK_DIRECT=1: per-output energy sums, A/B)
+    const bool direct = ofs::variant_on(ofs::V_PARK_DIRECT);
     auto k = (half >= OPT - 1 && !direct) ? park_kernel<FMT, R, true> : park_kernel<FMT, R, false>;
     const int rc = set_lds(k, lds);
     if (rc) return rc;
@@ -992,9 +992,8 @@ static bool zw64_args(const ZfArgs& a, Zw64Args& z) {
     }
     return true;
 }
-static bool zw64_enabled() {            // OFS_ZW64=0 forces zc_win_kernel (A/B timing)
-    const char* s = getenv("OFS_ZW64");
-    return !(s && s[0] == '0');
+static bool zw64_enabled() {            // variant ZW64=0 forces zc_win_kernel (A/B timing)
+    return !ofs::variant_off(ofs::V_ZW64);
 }
 static int zw64_launch(const Zw64Args& z, int nb, hipStream_t st) {
     const int rc = set_lds(zc_win64_kernel, Z64_LDS);
@@ -1003,11 +1002,11 @@ static int zw64_launch(const Zw64Args& z, int nb, hipStream_t st) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return OFS_EHIP;
-    // persistent grid: one 160 KiB workgroup per CU (OFS_ZW64_GRID overrides, for tuning)
+    // persistent grid: one 160 KiB workgroup per CU (variant ZW64_GRID overrides, for tuning)
     const int64_t items = z.B * z.noff;
     int64_t grid = (items + Z64_WAVES - 1) / Z64_WAVES;
-    const char* g = getenv("OFS_ZW64_GRID");
-    const int64_t cap = g ? atoll(g) : cus;
+    const int64_t gv = ofs::variant_or(ofs::V_ZW64_GRID, 0);
+    const int64_t cap = gv > 0 ? gv : cus;
     if (grid > cap) grid = cap;
     hipLaunchKernelGGL(zc_win64_kernel, dim3((unsigned)grid), dim3(64 * Z64_WAVES), Z64_LDS, st, z, nb);
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
@@ -1093,9 +1092,8 @@ extern "C" int ofs_zc_slide_ok(int fmt, int n_br, int N, int nbins, int64_t noff
 extern "C" int ofs_zc_slide_launch(int fmt, int n_br, int out_f32, const void* x, int64_t B, int64_t T, int N, int cp,
                                    int nbins, const int* kb, const double* tr, const double* ti, double t_energy,
                                    void* metric, hipStream_t st);
-static bool zs_enabled() {                 // OFS_ZS=0: the earlier one-chunk-per-wave kernel (A/B)
-    const char* s = getenv("OFS_ZS");
-    return !(s && s[0] == '0');
+static bool zs_enabled() {                 // variant ZS=0: the earlier one-chunk-per-wave kernel (A/B)
+    return !ofs::variant_off(ofs::V_ZS);
 }
 
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
@@ -1138,8 +1136,9 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
         if (r != 0) return r == 1 ? OFS_OK : r;
     }
     if (n_br > 4) return OFS_EINVAL;
-    // chunks of offsets: halve from ~N while the grid has fewer than OFS_ZF_ITEMS chunks in all
-    static const int64_t zf_items = getenv("OFS_ZF_ITEMS") ? atoll(getenv("OFS_ZF_ITEMS")) : 4096;
+    // chunks of offsets: halve from ~N while the grid has fewer than 4096 chunks in all (variant ZF_ITEMS)
+    const int64_t zfv = ofs::variant_or(ofs::V_ZF_ITEMS, 4096);
+    const int64_t zf_items = zfv > 0 ? zfv : 4096;
     int64_t chunk = ((std::max<int64_t>(N, 256) + 63) / 64) * 64;
     while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < zf_items) chunk = ((chunk / 2 + 63) / 64) * 64;
     a.chunk = chunk;

@@ -18,6 +18,8 @@
 #include <math.h>
 #include "ofdmsync.h"
 #include "ofs_common.h"
+#include <atomic>
+#include <string.h>
 
 namespace {
 
@@ -811,6 +813,39 @@ int32_t ofs_version(void) { return 100; }
 // in a one-line translation unit __graft_entry__.build_hip generates, so a source edit does not
 // force this file to recompile.
 
+static const char* const kVariantNames[ofs::V_COUNT] = {
+    "EXACT", "FAST_E", "FAST_E_DO", "FAST_SCAN", "FAST_SCAN_DO", "RTL_WPB", "PARK_DIRECT", "ZW64",
+    "ZW64_GRID", "ZS", "ZF_ITEMS", "ZS_PAIR", "ZS_DEFER", "ZS_BPL", "ZS_C", "ZS_GBLK", "MC_FUSED",
+    "MC_FUSE_X", "ZC_SEQ", "ZC_NODMA", "BE_FAST"};
+static std::atomic<int64_t> g_variants[ofs::V_COUNT] = {};
+static std::atomic<bool> g_variants_init{false};
+
+static int variant_index(const char* name) {
+    if (!name) return -1;
+    for (int i = 0; i < ofs::V_COUNT; ++i)
+        if (strcmp(name, kVariantNames[i]) == 0) return i;
+    return -1;
+}
+
+int32_t ofs_debug_reset_variants(void) {
+    for (auto& v : g_variants) v.store(OFS_VARIANT_UNSET, std::memory_order_relaxed);
+    g_variants_init.store(true, std::memory_order_release);
+    return OFS_OK;
+}
+
+int32_t ofs_debug_set_variant(const char* name, int64_t value) {
+    const int i = variant_index(name);
+    if (i < 0) return OFS_EINVAL;
+    if (!g_variants_init.load(std::memory_order_acquire)) ofs_debug_reset_variants();
+    g_variants[i].store(value, std::memory_order_relaxed);
+    return OFS_OK;
+}
+
+int64_t ofs_debug_get_variant(const char* name) {
+    const int i = variant_index(name);
+    return i < 0 ? OFS_VARIANT_UNSET : ofs::variant((ofs::Variant)i);
+}
+
 const char* ofs_status_string(int32_t s) {
     switch (s) {
         case OFS_OK: return "ok";
@@ -1052,3 +1087,10 @@ int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64
 }
 
 }  // extern "C"
+
+namespace ofs {
+int64_t variant(Variant v) {
+    if (!g_variants_init.load(std::memory_order_acquire)) return OFS_VARIANT_UNSET;
+    return g_variants[v].load(std::memory_order_relaxed);
+}
+}  // namespace ofs

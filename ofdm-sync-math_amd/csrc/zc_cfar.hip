@@ -459,12 +459,12 @@ int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double 
                     double* thresh_scaled, uint8_t* above, uint8_t* valid, uint8_t* gate_mask, int max_ev,
                     int32_t* n_ev, int64_t* ev, double* ev_v, hipStream_t st) {
     const int Hp = hyst > 1 ? hyst : 1;
-    if (Hp < 64 || B <= 0 || n <= 0 || getenv("OFS_ZC_SEQ")) return 0;
+    if (Hp < 64 || B <= 0 || n <= 0 || ofs::variant_on(ofs::V_ZC_SEQ)) return 0;
     ZcArgs a{corr_mag, B, n, W, tv, scale, minmag, reflen, Hp, local_sum, corr_scaled, thresh_scaled,
              above, valid, gate_mask, max_ev, n_ev, ev, ev_v};
     constexpr int SD = OFS_ZC_S, HD = OFS_ZC_H, SR = OFS_ZC_S_REG, HR = OFS_ZC_H_REG;
     const bool dma = ZC % 128 == 0 && n % ZC == 0 && W % ZC == 0 && W >= 0 &&
-                     (reinterpret_cast<uintptr_t>(corr_mag) & 15) == 0 && !getenv("OFS_ZC_NODMA");
+                     (reinterpret_cast<uintptr_t>(corr_mag) & 15) == 0 && !ofs::variant_on(ofs::V_ZC_NODMA);
     if (dma) hipLaunchKernelGGL((zc_cfar_kernel<true, SD, HD>), dim3((unsigned)((B + SD - 1) / SD)), dim3(64 * (1 + HD)), 0, st, a);
     else hipLaunchKernelGGL((zc_cfar_kernel<false, SR, HR>), dim3((unsigned)((B + SR - 1) / SR)), dim3(64 * (1 + HR)), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include "ofdmsync.h"
+#include "ofs_common.h"
 
 namespace {
 
@@ -332,13 +333,11 @@ __global__ void mc_prep_kernel(const double2* H, double2* Hbr, int M, int lb) {
     }
 }
 
-bool mc_fused_enabled() {                       // OFS_MC_FUSED=0: the rocFFT pipeline (A/B)
-    const char* e = getenv("OFS_MC_FUSED");
-    return !(e && atoi(e) == 0);
+bool mc_fused_enabled() {                       // variant MC_FUSED=0: the rocFFT pipeline (A/B)
+    return !ofs::variant_off(ofs::V_MC_FUSED);
 }
-bool mc_fuse_extract() {                        // OFS_MC_FUSE_X=0: scratch + extract kernel (A/B)
-    const char* e = getenv("OFS_MC_FUSE_X");
-    return !(e && atoi(e) == 0);
+bool mc_fuse_extract() {                        // variant MC_FUSE_X=0: scratch + extract kernel (A/B)
+    return !ofs::variant_off(ofs::V_MC_FUSE_X);
 }
 
 // inclusive block scan of per-thread sums (fp64), returns the exclusive prefix of this thread

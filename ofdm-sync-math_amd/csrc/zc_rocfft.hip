@@ -248,8 +248,8 @@ int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows,
                                                                       : HIP_SYMBOL(zc_store_cb_f64_ptr),
                                       sizeof(void*)) == hipSuccess && p->cb_fn;
         if (!ok) {
-            if (p->cb_dev) hipFree(p->cb_dev);
-            if (p->cb_host) hipHostFree(p->cb_host);
+            if (p->cb_dev) (void)hipFree(p->cb_dev);
+            if (p->cb_host) (void)hipHostFree(p->cb_host);
             rocfft_plan_destroy(p->plan);
             if (p->tail) rocfft_plan_destroy(p->tail);
             delete p;
@@ -271,8 +271,8 @@ int32_t ofs_zc_fft_plan_destroy(void* plan) {
     if (!p) return OFS_OK;
     if (p->plan) rocfft_plan_destroy(p->plan);
     if (p->tail) rocfft_plan_destroy(p->tail);
-    if (p->cb_dev) hipFree(p->cb_dev);
-    if (p->cb_host) hipHostFree(p->cb_host);
+    if (p->cb_dev) (void)hipFree(p->cb_dev);
+    if (p->cb_host) (void)hipHostFree(p->cb_host);
     delete p;
     return OFS_OK;
 }

@@ -617,16 +617,15 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
 
 namespace {
 // Row sums: deferred LDS partials for one branch, per-step DPP for two (measured, profiles/r03l_*:
-// one branch 0.188 -> 0.183 ms, two branches 0.796 -> 0.840 ms); OFS_ZS_DEFER=0|1 forces either (A/B)
+// one branch 0.188 -> 0.183 ms, two branches 0.796 -> 0.840 ms); variant ZS_DEFER=0|1 forces either (A/B)
 bool zs_defer(int n_br) {
-    const char* s = getenv("OFS_ZS_DEFER");
-    return s ? atoi(s) != 0 : n_br == 1;
+    const int64_t v = ofs::variant(ofs::V_ZS_DEFER);
+    return v != INT64_MIN ? v != 0 : n_br == 1;
 }
 
-// OFS_ZS_PAIR=0: the per-bin kernel even for a paired template (A/B)
+// variant ZS_PAIR=0: the per-bin kernel even for a paired template (A/B)
 bool zs_pair_enabled() {
-    const char* s = getenv("OFS_ZS_PAIR");
-    return !(s && atoi(s) == 0);
+    return !ofs::variant_off(ofs::V_ZS_PAIR);
 }
 
 template <class K>
@@ -690,18 +689,17 @@ bool zs_pairs(ZsArgs& a) {
 namespace {
 // chunk / block length C (C | N; 256 for N >= 8192 keeps the blocks per window at <= 32), waves per
 // workgroup W (<= 16; 8 for two branches) and the workgroup's LDS; false if the blocks do not fit
-// bins per lane of the slide: 8 for one branch (OFS_ZS_BPL=4 for the A/B), 4 for two (8 would
+// bins per lane of the slide: 8 for one branch (variant ZS_BPL=4 for the A/B), 4 for two (8 would
 // exceed the 128 VGPRs of a 16-wave workgroup and spill)
 int zs_bpl(int n_br) {
-    const char* s = getenv("OFS_ZS_BPL");
-    return (n_br == 2 || (s && atoi(s) == 4)) ? 4 : 8;
+    return (n_br == 2 || ofs::variant_is(ofs::V_ZS_BPL, 4)) ? 4 : 8;
 }
 
 bool zs_plan(int n_br, int N, int bpl, int& C, int& W, size_t& lds, int64_t noff) {
     C = (N >= 8192 && N % 256 == 0) ? 256 : (N % 128 == 0 ? 128 : 64);
-    if (const char* e = getenv("OFS_ZS_C")) {                         // A/B: chunk length override
-        const int c = atoi(e);
-        if (c >= 64 && c <= 256 && c % 64 == 0 && N % c == 0) C = c;
+    {                                                                  // A/B: chunk length override
+        const int64_t c = ofs::variant(ofs::V_ZS_C);
+        if (c >= 64 && c <= 256 && c % 64 == 0 && N % c == 0) C = (int)c;
     }
     const int64_t nchunks = (noff + C - 1) / C;
     W = (int)std::min<int64_t>(n_br == 1 ? 16 : 8, (nchunks + bpl - 1) / bpl);
@@ -747,10 +745,7 @@ extern "C" int ofs_zc_slide_launch(int fmt, int n_br, int out_f32, const void* x
     if (a.B * a.groups > 0x7fffffff) return 0;
     const bool f = out_f32 != 0;
     a.npairs = 0;
-    {
-        const char* e = getenv("OFS_ZS_GBLK");                     // 0: Horner block DFTs in the pair kernel (A/B)
-        a.gblk = !(e && atoi(e) == 0);
-    }
+    a.gblk = !ofs::variant_off(ofs::V_ZS_GBLK);                     // 0: Horner block DFTs in the pair kernel (A/B)
     const bool pair = zs_pair_enabled() && bpl == (n_br == 2 ? 4 : 8) && zs_pairs(a);
 #define ZS_CASE(F, NBV) \
     if (fmt == F && n_br == NBV) \

@@ -127,6 +127,9 @@ def _declare(lib):
                                     c_int32, P, P, P, P, P, P, c_int32, P, P, P, P]),
         "ofs_zc_gate": (c_int32, [P, P, P, c_int64, c_int64, c_int32, c_int32, P, c_int32, P, P, P,
                                   P]),
+        "ofs_debug_set_variant": (c_int32, [ctypes.c_char_p, c_int64]),
+        "ofs_debug_get_variant": (c_int64, [ctypes.c_char_p]),
+        "ofs_debug_reset_variants": (c_int32, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -155,6 +158,49 @@ def lib():
         _declare(l)
         _lib = l
     return _lib
+
+
+# ------------------------------------------------------------------------------------------
+# debug / A-B variants (include/ofdmsync.h ofs_debug_set_variant): the library reads no
+# environment; tests and measurement tools force an alternative kernel through this entry only
+# ------------------------------------------------------------------------------------------
+VARIANT_UNSET = -(1 << 63)
+
+
+def set_variant(name: str, value) -> None:
+    """Force (value: int) or clear (value None) one debug variant, e.g. set_variant("EXACT", 0)."""
+    rc = lib().ofs_debug_set_variant(name.encode(), VARIANT_UNSET if value is None else int(value))
+    if rc != 0:
+        raise ValueError(f"unknown variant {name!r}")
+
+
+def get_variant(name: str):
+    v = lib().ofs_debug_get_variant(name.encode())
+    return None if v == VARIANT_UNSET else int(v)
+
+
+def reset_variants() -> None:
+    lib().ofs_debug_reset_variants()
+
+
+class variants:
+    """Context manager: ``with variants(EXACT=0, FAST_E=4): ...`` sets the variants for the block
+    and restores the previous values after it."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.prev[k] = get_variant(k)
+            set_variant(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            set_variant(k, v)
+        return False
 
 
 def require_gpu() -> torch.device:

@@ -66,7 +66,9 @@ class AABatchResult:
 
     P [B,T] complex, R/M [B,T] real, valid [B,T] bool (None when not requested);
     n_events [B] int32; ev_int [B,E,4] int64 = (peak_index, gate_start, gate_end, frame_start);
-    ev_real [B,E,4] f64 = (P_re, P_im, M_at_peak, cfo_hz); E = max_events.
+    ev_real [B,E,4] f64 = (P_re, P_im, M_at_peak, cfo_hz); E = max_events.  Only the first
+    min(n_events[b], E) slots of stream b are written; the rest are undefined (the buffers are
+    not cleared per call: ``live_events`` gives the mask).
     """
     P: torch.Tensor | None
     R: torch.Tensor | None
@@ -75,6 +77,11 @@ class AABatchResult:
     n_events: torch.Tensor | None
     ev_int: torch.Tensor | None
     ev_real: torch.Tensor | None
+
+
+def live_events(n_events: torch.Tensor, E: int) -> torch.Tensor:
+    """[B, E] bool mask of the event slots a call wrote (slot j of stream b iff j < n_events[b])."""
+    return torch.arange(E, device=n_events.device)[None, :] < n_events.to(torch.int64)[:, None]
 
 
 def quantize_adc(samples, full_scale: float, bits: int = ADC_BITS):
@@ -136,9 +143,11 @@ def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_ra
                                 ((B, T), torch.bool) if "valid" in want else None], placement)
     n_ev = ev_i = ev_r = None
     if detect:
-        n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
-        ev_i = torch.zeros((B, max(max_events, 1), 4), dtype=torch.int64, device=dev)
-        ev_r = torch.zeros((B, max(max_events, 1), 4), dtype=torch.float64, device=dev)
+        # every stream's count is written by the kernel; event slots past it are not, and are
+        # left uninitialised (no per-call memset of 2 x B x E x 32 B; readers mask with live_events)
+        n_ev = torch.empty((B,), dtype=torch.int32, device=dev)
+        ev_i = torch.empty((B, max(max_events, 1), 4), dtype=torch.int64, device=dev)
+        ev_r = torch.empty((B, max(max_events, 1), 4), dtype=torch.float64, device=dev)
     rc = _lib.lib().ofs_aa_detect(batch.fmt, batch.data.data_ptr(), B, batch.nb, T, int(L), prec,
                                   _lib.ptr(P), _lib.ptr(R), _lib.ptr(M), _lib.ptr(V), int(detect),
                                   float(threshold), int(hysteresis), float(sample_rate),

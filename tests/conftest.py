@@ -18,3 +18,14 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture
+def variant():
+    """Setter of the library's debug / A-B variants (include/ofdmsync.h ofs_debug_set_variant):
+    ``variant("EXACT", 0)`` forces one, ``variant("EXACT", None)`` clears it; all are cleared
+    after the test.  The library reads no environment, so this is the only way to select one."""
+    from ofdm_sync_amd import _lib
+    _lib.reset_variants()
+    yield _lib.set_variant
+    _lib.reset_variants()

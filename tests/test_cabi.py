@@ -112,3 +112,36 @@ def test_product_path_refuses_cpu():
     from ofdm_sync_amd import sync_aa
     with pytest.raises(RuntimeError, match="GPU"):
         sync_aa.aa_detect_streaming([1 + 1j] * 32, L=4)
+
+
+def test_library_reads_no_environment():
+    """Dispatch and arithmetic depend only on the call's arguments (and on debug variants set
+    through ofs_debug_set_variant): no source of the shipped library calls getenv / secure_getenv."""
+    csrc = os.path.join(ROOT, "ofdm-sync-math_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        txt = open(os.path.join(csrc, f)).read()
+        assert not re.search(r"\b(secure_)?getenv\s*\(", txt), f
+    out = os.popen(f"nm -D --undefined-only {LIB}").read()
+    assert not re.search(r"\bU\s+(secure_)?getenv\b", out)
+
+
+def test_debug_variants_entry_point(lib):
+    """ofs_debug_set_variant / _get_variant / _reset_variants: unknown names refused, values
+    round-trip, reset clears every variant, and the default is unset."""
+    from ofdm_sync_amd import _lib as L
+    L._declare(lib)
+    unset = -(1 << 63)
+    assert lib.ofs_debug_reset_variants() == 0
+    hdr = open(HEADER).read()
+    block = hdr[hdr.index("Names (value meaning):"):hdr.index("ofs_debug_set_variant returns")]
+    names = re.findall(r"^ \*   ([A-Z][A-Z0-9_]+)\s", block, re.M)
+    assert {"EXACT", "MC_FUSED", "ZS_PAIR", "FAST_SCAN", "BE_FAST", "ZC_SEQ"} <= set(names)
+    for n in names:
+        assert lib.ofs_debug_get_variant(n.encode()) == unset, n
+        assert lib.ofs_debug_set_variant(n.encode(), 7) == 0, n
+        assert lib.ofs_debug_get_variant(n.encode()) == 7, n
+    assert lib.ofs_debug_set_variant(b"NO_SUCH_KNOB", 1) == -1
+    assert lib.ofs_debug_get_variant(b"NO_SUCH_KNOB") == unset
+    assert lib.ofs_debug_set_variant(b"EXACT", unset) == 0 and lib.ofs_debug_get_variant(b"EXACT") == unset
+    assert lib.ofs_debug_reset_variants() == 0
+    assert all(lib.ofs_debug_get_variant(n.encode()) == unset for n in names)

@@ -295,7 +295,7 @@ def test_zc_freq_fp32_window_fft_vs_oracle(N, cp, T, nb):
 
 
 @pytest.mark.parametrize("B,nb,cp,T", [(1500, 1, 0, 4096), (300, 2, 1, 4099), (70, 3, 6, 4110)])
-def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, monkeypatch):
+def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, variant):
     """N = 4096 lane-reduce kernel (plan 3): persistent grid (B*noff > resident waves), multiple
     branches, odd window starts (direct-load fallback next to the LDS-DMA prefetch).  Against the
     oracle (every stream, error model 2) with both kernels."""
@@ -312,7 +312,7 @@ def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, monkeypatch):
     xd = torch.from_numpy(x).cuda()
     assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 3
     m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp).cpu().numpy()
-    monkeypatch.setenv("OFS_ZW64", "0")
+    variant("ZW64", 0)
     assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, T, N, cp) == 2
     m2 = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp).cpu().numpy()
     for mm, name in ((m, "lane-reduce"), (m2, "transpose")):
@@ -352,10 +352,10 @@ def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
                                            ("c128", 64, 16, 700, 1), ("c128", 4096, 1024, 9000, 1),
                                            ("c128", 8192, 0, 8300, 1), ("c128", 192, 5, 1000, 2),
                                            ("c128", 2048, 512, 2600, 1)])
-def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
+def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, variant):
     """The block-initialised sliding DFT (zc_slide.hip, plan 4: the pair resonators for the ZC template's
     ±k bins) against the C oracle's fp64 FFTs on every window (1e-9 relative + 1e-11), against the
-    per-bin recursion (OFS_ZS_PAIR=0) and the earlier one-chunk-per-wave kernel (OFS_ZS=0):
+    per-bin recursion (variant ZS_PAIR=0) and the earlier one-chunk-per-wave kernel (variant ZS=0):
     odd T, cp offsets, chunks past the end, N not a power of two (192), N = 8192 (256-sample
     blocks), offsets fewer than one chunk (T = 2600), int16 and complex64 input, two branches."""
     from ofdm_sync_amd import _lib
@@ -375,17 +375,17 @@ def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
     assert _lib.lib().ofs_zc_freq_plan({"c128": _lib.C128, "c64": _lib.C64, "i16": _lib.CI16}[fmt], _lib.FP64, T, N,
                                        cp) == 4
     m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.setenv("OFS_ZS", "0")
+    variant("ZS", 0)
     m_prev = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.delenv("OFS_ZS")
+    variant("ZS", None)
     np.testing.assert_allclose(m, m_prev, rtol=1e-9, atol=1e-11)
-    monkeypatch.setenv("OFS_ZS_DEFER", "0")        # per-step DPP row sums instead of the LDS partials
+    variant("ZS_DEFER", 0)        # per-step DPP row sums instead of the LDS partials
     m_dpp = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.delenv("OFS_ZS_DEFER")
+    variant("ZS_DEFER", None)
     np.testing.assert_allclose(m, m_dpp, rtol=1e-12, atol=1e-14)
-    monkeypatch.setenv("OFS_ZS_PAIR", "0")         # first-order recursion per bin instead of the pair resonators
+    variant("ZS_PAIR", 0)         # first-order recursion per bin instead of the pair resonators
     m_bin = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.delenv("OFS_ZS_PAIR")
+    variant("ZS_PAIR", None)
     np.testing.assert_allclose(m, m_bin, rtol=1e-9, atol=1e-11)
     for b in range(B):
         mo = O.zc_freq_metric(np.asarray(x[b], np.complex128), N, cp, idx, t, e)
@@ -394,12 +394,12 @@ def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, monkeypatch):
 
 @pytest.mark.parametrize("tmpl,nb", [("zc_shuffled", 1), ("random_pairs", 1), ("random_pairs", 2),
                                      ("unpaired", 1), ("with_dc", 2), ("one_pair", 1)])
-def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
+def test_zc_slide_templates_pair_and_fallback(tmpl, nb, variant):
     """Template shapes around the pair kernel's condition (every bin k has its mirror N - k, neither
     0 nor N/2): ZC bins in shuffled slot order, random complex template values on paired bins (the
     A/B constants), an unpaired set and a set with the DC bin (both take the per-bin recursion), a
     single pair.  Each against the C oracle's direct DFT (1e-9 relative + 1e-11) and the per-bin
-    kernel (OFS_ZS_PAIR=0)."""
+    kernel (variant ZS_PAIR=0)."""
     from ofdm_sync_amd import _lib
     N, cp, T = 2048, 512, 6000
     rng = np.random.default_rng(hash(tmpl) % 1000 + nb)
@@ -424,9 +424,9 @@ def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
     x[0, :, 700:700 + N] += 3 * O.pss_symbol(N)
     xd = torch.from_numpy(x).cuda()
     m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.setenv("OFS_ZS_PAIR", "0")
+    variant("ZS_PAIR", 0)
     m_bin = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
-    monkeypatch.delenv("OFS_ZS_PAIR")
+    variant("ZS_PAIR", None)
     np.testing.assert_allclose(m, m_bin, rtol=1e-9, atol=1e-11)
     for b in range(2):
         np.testing.assert_allclose(m[b], O.zc_freq_metric(x[b], N, cp, idx, t, e), rtol=1e-9, atol=1e-11)
@@ -436,11 +436,11 @@ def test_zc_slide_templates_pair_and_fallback(tmpl, nb, monkeypatch):
 @pytest.mark.parametrize("fmt,nb,N,T", [("c128", 1, 2048, 16384), ("c128", 2, 2048, 7000), ("c64", 3, 1024, 3000),
                                         ("int16", 2, 512, 2500), ("c128", 1, 2048, 1000), ("c128", 2, 256, 40),
                                         ("c64", 1, 2048, 9000), ("int16", 1, 2048, 12000)])
-def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, monkeypatch):
+def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, variant):
     """FFT overlap-save matched filter (ofs_zc_correlate_fft) against the direct sums on the same
     samples, every combine mode: corr within 1e-11 of the row maximum, |corr| 1e-9 relative; for
     8192-point blocks both the fused LDS-FFT kernel (default) and the rocFFT pipeline
-    (OFS_MC_FUSED=0)."""
+    (variant MC_FUSED=0)."""
     rng = np.random.default_rng(N + T + nb)
     B = 3
     x = rng_c(rng, B, nb, T) * 100
@@ -452,7 +452,7 @@ def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, monkeypatch):
     else:
         xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
     for fused in ("1", "0"):
-        monkeypatch.setenv("OFS_MC_FUSED", fused)
+        variant("MC_FUSED", int(fused))
         for mode in (zc_v2.OFS_ZC_RAW, zc_v2.OFS_ZC_V2, zc_v2.OFS_ZC_COMBINED, zc_v2.OFS_ZC_SUM):
             cf, mf = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
             cd, md = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="direct")
@@ -460,7 +460,7 @@ def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, monkeypatch):
             scale = np.abs(cd).max(axis=-1, keepdims=True)
             assert np.max(np.abs(cf - cd) / scale) < 1e-11, (mode, fused)
             np.testing.assert_allclose(mf, md, rtol=1e-9, atol=1e-11 * float(scale.max()))
-    monkeypatch.delenv("OFS_MC_FUSED")
+    variant("MC_FUSED", None)
 
 
 def test_zc_detect_four_branches_n2048_falls_back_to_direct():

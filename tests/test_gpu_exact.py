@@ -1,7 +1,7 @@
 """Integer-exact wave-per-stream kernels (csrc/aa_exact.hip) for int16 I/Q input.
 
 For int16 samples every product and window sum is an exact integer, so the exact kernels and
-the general LDS engine (forced with OFS_EXACT=0) must agree BIT FOR BIT although they sum in
+the general LDS engine (forced with variant EXACT=0) must agree BIT FOR BIT although they sum in
 different orders: P, R, M, valid and the events of sync_aa (sync_aa.py:421-571); all eight
 arrays and the gate events of minn_rtl (minn_rtl.py:583-825).  Integer arrays are also checked
 against the CPU oracle (bit-exact), which is itself pinned to the reference's goldens.
@@ -39,8 +39,8 @@ def _int12_bursts(rng, B, nb, T, blocks, amp=1500, noise=60):
     return np.stack([re, im], axis=-1).astype(np.int16)
 
 
-def _aa_run(xt, L, monkeypatch, exact: bool):
-    monkeypatch.setenv("OFS_EXACT", "1" if exact else "0")
+def _aa_run(xt, L, variant, exact: bool):
+    variant("EXACT", 1 if exact else 0)
     out = sync_aa.aa_detect_streaming_batched(xt, L=L, threshold=0.15, hysteresis=16)
     torch.cuda.synchronize()
     return out
@@ -48,14 +48,14 @@ def _aa_run(xt, L, monkeypatch, exact: bool):
 
 @pytest.mark.parametrize("B,nb,T,L", [(37, 1, 1024, 128), (9, 2, 999, 256), (5, 1, 5000, 512),
                                       (6, 2, 700, 64), (3, 1, 2300, 1024)])
-def test_aa_exact_kernel_bit_identical_to_general_engine(B, nb, T, L, monkeypatch):
+def test_aa_exact_kernel_bit_identical_to_general_engine(B, nb, T, L, variant):
     rng = np.random.default_rng(B * 7 + L)
     iq = _int12_bursts(rng, B, nb, T, ([1, 1], np.zeros(L)))
     xt = torch.from_numpy(iq).cuda()
     plan = _lib.lib().ofs_aa_plan(_lib.CI16, _lib.FP64, nb, T, L)
     assert 2000 < plan < 3000, plan                    # the exact kernel serves this shape
-    a = _aa_run(xt, L, monkeypatch, True)
-    g = _aa_run(xt, L, monkeypatch, False)
+    a = _aa_run(xt, L, variant, True)
+    g = _aa_run(xt, L, variant, False)
     for k in ("P", "R", "M", "valid", "n_events"):
         assert torch.equal(getattr(a, k), getattr(g, k)), k
     n = a.n_events.cpu().numpy()
@@ -72,8 +72,8 @@ def test_aa_exact_kernel_bit_identical_to_general_engine(B, nb, T, L, monkeypatc
         assert np.array_equal(a.valid[b].cpu().numpy(), v)
 
 
-def _rtl_run(xt, Q, monkeypatch, exact, **kw):
-    monkeypatch.setenv("OFS_EXACT", "1" if exact else "0")
+def _rtl_run(xt, Q, variant, exact, **kw):
+    variant("EXACT", 1 if exact else 0)
     out = minn_rtl.minn_rtl_batched(xt, Q, **kw)
     torch.cuda.synchronize()
     return out
@@ -82,15 +82,15 @@ def _rtl_run(xt, Q, monkeypatch, exact, **kw):
 @pytest.mark.parametrize("B,nb,T,Q", [(33, 1, 1024, 64), (7, 2, 777, 64), (5, 3, 3000, 128),
                                       (4, 1, 4096, 512), (6, 2, 2500, 256)])
 @pytest.mark.parametrize("mode,shift,hyst", [("float", 3, 2), ("floor", 3, 2), ("float", 0, 0), ("floor", 0, 1), ("floor", 6, 3)])
-def test_rtl_exact_kernel_bit_identical_to_general_engine(B, nb, T, Q, mode, shift, hyst, monkeypatch):
+def test_rtl_exact_kernel_bit_identical_to_general_engine(B, nb, T, Q, mode, shift, hyst, variant):
     rng = np.random.default_rng(B + Q + shift)
     iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q)))
     xt = torch.from_numpy(iq).cuda()
     assert _lib.lib().ofs_rtl_plan(_lib.CI16, nb, T, Q) > 2000
     kw = dict(smooth_shift=shift, threshold_value=3276, threshold_frac_bits=15, smooth_mode=mode,
               hysteresis=hyst, timing_offset=-5)
-    a = _rtl_run(xt, Q, monkeypatch, True, **kw)
-    g = _rtl_run(xt, Q, monkeypatch, False, **kw)
+    a = _rtl_run(xt, Q, variant, True, **kw)
+    g = _rtl_run(xt, Q, variant, False, **kw)
     for k in RTL_KEYS + ("n_events", "open_gate_start"):
         assert torch.equal(getattr(a, k), getattr(g, k)), k
     n = a.n_events.cpu().numpy()
@@ -106,7 +106,7 @@ def test_rtl_exact_kernel_bit_identical_to_general_engine(B, nb, T, Q, mode, shi
     assert np.array_equal(a.events[0, :int(n[0])].cpu().numpy(), ev)
 
 
-def test_rtl_exact_metric_only_outputs(monkeypatch):
+def test_rtl_exact_metric_only_outputs():
     """Metric without smoothing outputs or gate (the optional arrays of ofs_minn_rtl are null
     except corr_total / energy_total): exact kernel skips the sequential pass."""
     rng = np.random.default_rng(3)
@@ -134,7 +134,7 @@ def test_exact_plans_fall_back_outside_exact_range():
 
 @pytest.mark.parametrize("shift", [1, 2, 3, 5, 8])
 @pytest.mark.parametrize("T", [1024, 2100, 513])
-def test_rtl_segment_parallel_iir_is_exact(shift, T, monkeypatch):
+def test_rtl_segment_parallel_iir_is_exact(shift, T, variant):
     """The segment-parallel IIR (aa_exact.hip: guessed chunk states, exact chunk runs iterated
     to a self-consistent chain) equals the general engine's sequential recursion and the
     oracle bit for bit, across contraction factors and partial segments."""
@@ -144,8 +144,8 @@ def test_rtl_segment_parallel_iir_is_exact(shift, T, monkeypatch):
     xt = torch.from_numpy(iq).cuda()
     kw = dict(smooth_shift=shift, threshold_value=3276, threshold_frac_bits=15, smooth_mode="float",
               hysteresis=2, timing_offset=0)
-    a = _rtl_run(xt, Q, monkeypatch, True, **kw)
-    g = _rtl_run(xt, Q, monkeypatch, False, **kw)
+    a = _rtl_run(xt, Q, variant, True, **kw)
+    g = _rtl_run(xt, Q, variant, False, **kw)
     for k in RTL_KEYS + ("n_events", "open_gate_start"):
         assert torch.equal(getattr(a, k), getattr(g, k)), k
     xc = (iq[1, ..., 0] + 1j * iq[1, ..., 1]).astype(np.complex128)

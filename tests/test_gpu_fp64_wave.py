@@ -1,6 +1,6 @@
 """The fp64 wave-per-stream sync_aa path for complex128 input (aa_exact_kernel<OFS_C128>, plan
 3000 + 10*E + MR, any T): the numpy drop-in's arithmetic (sync_aa.py:421-571 in float64).  Checked
-against the CPU oracle and against the general LDS engine (OFS_EXACT=0 routes the same call
+against the CPU oracle and against the general LDS engine (variant EXACT=0 routes the same call
 there) on ragged lengths, one and two antennas, every supported L, and a loud burst next to a
 quiet window.
 
@@ -38,15 +38,15 @@ def _rel(a, b):
 @pytest.mark.parametrize("T,L,na", [(1024, 512, 1), (1023, 512, 1), (3584, 1024, 1), (2024, 512, 2),
                                     (777, 128, 2), (300, 64, 1), (1, 64, 1), (130, 256, 1),
                                     (5315, 512, 2), (9000, 512, 1), (16384, 256, 1)])
-def test_fp64_wave_vs_general_engine_and_oracle(T, L, na, monkeypatch):
+def test_fp64_wave_vs_general_engine_and_oracle(T, L, na, variant):
     B = 64
     x = _streams(B, na, T, L, seed=T + L)
     assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, na, T, L) > 3000
     got = sync_aa.aa_detect_streaming_batched(x, L)
-    monkeypatch.setenv("OFS_EXACT", "0")
+    variant("EXACT", 0)
     assert _lib.lib().ofs_aa_plan(_lib.C128, _lib.FP64, na, T, L) in (1, 2)
     ref = sync_aa.aa_detect_streaming_batched(x, L)
-    monkeypatch.delenv("OFS_EXACT")
+    variant("EXACT", None)
     for name, tol in (("P", 1e-11), ("R", 1e-11)):
         a, b = getattr(got, name).cpu().numpy(), getattr(ref, name).cpu().numpy()
         assert _rel(a, b) <= tol, name

@@ -524,9 +524,9 @@ def test_receiver_backend_vs_reference_golden(name):
 
 @pytest.mark.parametrize("fmt,nb,N", [("c64", 1, 2048), ("int16", 2, 1024), ("c128", 3, 256), ("c64", 2, 4096),
                                       ("c128", 2, 2048)])
-def test_receiver_backend_batched_vs_oracle(fmt, nb, N, monkeypatch):
+def test_receiver_backend_batched_vs_oracle(fmt, nb, N, variant):
     """The fused back-end (fast kernel for N = 1024 / 2048 / 4096 and 1-2 branches, the generic one
-    otherwise and under OFS_BE_FAST=0) against the oracle's chain, per frame."""
+    otherwise and under variant BE_FAST=0) against the oracle's chain, per frame."""
     rng = np.random.default_rng(N + nb)
     B, cp = 6, N // 4
     k = core.centered_subcarrier_indices(N // 2)
@@ -542,9 +542,9 @@ def test_receiver_backend_batched_vs_oracle(fmt, nb, N, monkeypatch):
     else:
         xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
     out = core.receiver_backend_batched(xd, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
-    monkeypatch.setenv("OFS_BE_FAST", "0")
+    variant("BE_FAST", 0)
     gen = core.receiver_backend_batched(xd, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
-    monkeypatch.delenv("OFS_BE_FAST")
+    variant("BE_FAST", None)
     for b in range(B):
         r = O.rx_backend(x[b], int(ps[b]), int(ds[b]), N, cp, 1e6, k, pil[b], dat)
         for o in (out, gen):

@@ -378,8 +378,8 @@ def cfg3_detect(dev, st, steps, warmup):
             0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
     ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa detect-only"), steps, warmup, st)
     stored = int(torch.clamp(n_ev, max=E).sum().item())
-    ed = int(os.environ.get("OFS_FAST_E_DO", "4"))
-    scan = "fp64" if os.environ.get("OFS_FAST_SCAN_DO", "32").startswith("6") else "fp32"
+    ed = _lib.get_variant("FAST_E_DO") or 4
+    scan = "fp64" if _lib.get_variant("FAST_SCAN_DO") == 64 else "fp32"
     return dict(config="cfg3_detect", workload=f"sync_aa S&C fp32 detect-only, L={L}, {B} x {T} c64 (events only)",
                 kernel=f"aa_fast_kernel<E={ed},MR={L // (64 * ed)},DO,{scan} row scans> (P/R/M stores off)",
                 samples=B * T, ms=ms,
@@ -563,21 +563,17 @@ def zc_freq_refshape(dev, st, steps, warmup, B=4096):
 def zc_detect(dev, st, steps, warmup, state=False, seq=False):
     """zc_v2 CFAR + gate (zc_v2.py:300-446) on |corr| rows: B = 4096 x 16384 f64.  Default kernel:
     zc_cfar_kernel (lane-per-stream exact recursion + closed-form gate, zc_cfar.hip); seq=True times
-    the sequential one-wave-per-stream kernel (OFS_ZC_SEQ).  state=True also stores the five state
+    the sequential one-wave-per-stream kernel (debug variant ZC_SEQ).  state=True also stores the five state
     arrays (local_sum, corr_scaled, thresh_scaled 8 B each, above, valid 1 B each)."""
     from ofdm_sync_amd import zc_v2
     B, n = 4096, 16384
     g = torch.Generator(device=dev).manual_seed(7)
     mag = torch.rand((B, n), dtype=torch.float64, device=dev, generator=g) * 0.5
     mag[:, 5000:5100] += 2.0
-    if seq:
-        os.environ["OFS_ZC_SEQ"] = "1"
-    try:
+    with _lib.variants(ZC_SEQ=1 if seq else None):
         ms = timed(lambda: zc_v2._detect_run(mag, zc_v2.CORR_WINDOW_SIZE, zc_v2.THRESH_VALUE, zc_v2.THRESH_FRAC_BITS,
                                              zc_v2.MIN_CORR_MAG, 2048, zc_v2.HYSTERESIS, 4, want_state=state),
                    steps, warmup, st)
-    finally:
-        os.environ.pop("OFS_ZC_SEQ", None)
     name = "zc_detect" + ("_state" if state else "") + ("_seq" if seq else "")
     return dict(config=name, workload=f"zc_v2 CFAR + gate, {B} x {n} f64 |corr| (events + gate mask"
                 + (" + state arrays)" if state else ")"),

@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ofdm-sync-math_amd"))
-from ofdm_sync_amd import zc_freq  # noqa: E402
+from ofdm_sync_amd import _lib, zc_freq  # noqa: E402
 
 
 def main():
@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--B", default="32,64,128,192,224,240,248,256,264,288,320,384,448,512,768,1024")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ab", default="", help="K=V[,K2=V2][;K=V...]: interleaved in-process A/B of knob sets the "
-                                             "library reads per launch (e.g. 'OFS_ZS_PAIR=0;OFS_ZS_PAIR=1'); "
+                                             "library reads per launch as debug variants (e.g. 'ZS_PAIR=0;ZS_PAIR=1'); "
                                              "medians of --reps")
     ap.add_argument("--reps", type=int, default=7)
     a = ap.parse_args()
@@ -53,17 +53,17 @@ def main():
             for _ in range(a.reps):
                 for i, st in enumerate(sets):
                     for k in keys:
-                        os.environ.pop(k, None)
-                    os.environ.update(st)
+                        _lib.set_variant(k.removeprefix("OFS_"), None)
+                    for k, v in st.items():
+                        _lib.set_variant(k.removeprefix("OFS_"), int(v))
                     run()
                     ts[i].append(run())
-            for k in keys:
-                os.environ.pop(k, None)
+            _lib.reset_variants()
             for i, st in enumerate(sets):
                 rec[",".join(f"{k}={v}" for k, v in st.items())] = round(sorted(ts[i])[len(ts[i]) // 2], 4)
         else:
             ms = run()
-            rec.update(ms=round(ms, 4), us_per_stream=round(1000 * ms / B, 3), defer=os.environ.get("OFS_ZS_DEFER", "1"))
+            rec.update(ms=round(ms, 4), us_per_stream=round(1000 * ms / B, 3), defer=_lib.get_variant("ZS_DEFER"))
         print(json.dumps(rec), flush=True)
 
 
