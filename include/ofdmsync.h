@@ -360,7 +360,10 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
  *     wave; N a multiple of 64, n_br <= 2), else the one-chunk-per-wave sliding DFT (n_br <= 4).
  *   OFS_FP32: few offsets per stream (<= 64, OFS_C64, N = 64*2^j <= 4096, the cfg5 shape): a
  *     per-window 64 x N/64 pruned FFT in fp32; otherwise the fp64 sliding DFT of zc_slide.hip with
- *     the metric rounded to fp32 (n_br <= 2, N a multiple of 64; else OFS_EINVAL).
+ *     the metric rounded to fp32 (n_br <= 2, N a multiple of 64, blocks within LDS), else the
+ *     one-chunk-per-wave fp64 sliding DFT with the metric rounded to fp32 (n_br <= 4).
+ *   n_br > 4: OFS_EINVAL (cover it, and templates of more than 64 bins, with ofs_zc_freq_partial
+ *     over branch / bin groups + ofs_zc_freq_finish, as the Python mirror does).
  * Returns OFS_ESHORT when T < N + cp (the reference raises ValueError).
  */
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
@@ -370,8 +373,24 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
 /* which zc_freq kernel a one-branch shape runs on: 1 one-chunk-per-wave sliding DFT (fp64), 2 window
  * FFT (fp32), 3 N = 4096 window FFT with the column sums reduced across lanes (fp32; taken when the
  * template bins' residues mod 64 are distinct, as the PSS template's are, otherwise 2), 4 block-
- * initialised sliding DFT (fp64), 5 the same with the metric rounded to fp32, 0 none */
+ * initialised sliding DFT (fp64), 5 the same with the metric rounded to fp32, 6 the one-chunk-per-
+ * wave sliding DFT with the metric rounded to fp32, 0 none */
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp);
+/* Partial sums of the zc_freq metric over one group of branches and one group of template bins, so
+ * any branch count and any template length reduce to kernels of <= 4 branches x <= 64 bins (the
+ * reference loops over every branch and bin, zc_freq.py:85-97).  For off in [0, noff), noff =
+ * T-(N+cp)+1, with bins b_{br,j} as in ofs_zc_freq_metric over branches br0 .. br0+n_grp-1 of x
+ * ([B][n_br][T]) and the n_bins (<= 64) given bins:
+ *   part[b][off] = (Re C, Im C, D),  C = Σ_br Σ_j conj(t_j)·b_{br,j},  D = Σ_br Σ_j |b_{br,j}|²
+ * stored, or added onto part when accumulate != 0 (part: [B][noff][3] f64, device).  The groups'
+ * C and D add exactly as the reference's per-branch vdot / energy sums do, before the one
+ * normalisation of ofs_zc_freq_finish.  fp64 sliding DFT (one chunk of offsets per wave). */
+int32_t ofs_zc_freq_partial(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T, int32_t br0,
+                            int32_t n_grp, int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
+                            const double* template_bins, int32_t accumulate, double* part, void* stream);
+/* metric[b][off] = |C|² / max(E_t·D, 1e-12) from accumulated partial sums; f32 (OFS_FP32) or f64 out. */
+int32_t ofs_zc_freq_finish(const double* part, int64_t B, int64_t noff, double template_energy,
+                           int32_t precision, void* metric, void* stream);
 
 /*
  * rocFFT leg of the ZC frequency-domain metric (zc_freq.py:62-99 and the argmax of

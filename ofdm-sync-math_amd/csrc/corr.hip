@@ -296,7 +296,11 @@ struct ZfArgs {
     const void* x; int64_t B, T; int N, cp; int64_t noff, chunk, nchunks;
     int nbins; double t_energy; void* metric;
     int kb[64]; double tr[64], ti[64];
+    int nb_all = 0, br0 = 0;          // zc_freq_kernel: branch rows b * nb_all + br0 + r (a branch group)
 };
+// zc_freq_kernel outputs: the metric in fp64 / fp32, or the partial sums (Re C, Im C, D) of a
+// branch / template-bin group stored or added onto [B][noff][3] f64 (ofs_zc_freq_partial)
+enum ZfOut : int { ZF_F64 = 0, ZF_F32 = 1, ZF_PART = 2, ZF_PART_ADD = 3 };
 
 __device__ __forceinline__ double quad_sum(double v) {
     v += ofs::dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -334,7 +338,7 @@ __device__ __forceinline__ void zf_window(const ZfArgs& a, int64_t b, int64_t s0
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
             double2 v = make_double2(0.0, 0.0);
-            if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * NB + r) * a.T + j0 + lane);
+            if (lane < cnt) v = ld_c<FMT, double>(a.x, (b * a.nb_all + a.br0 + r) * a.T + j0 + lane);
             xr[r] = v.x; xi[r] = v.y;
         }
         double2 tw[4];
@@ -381,7 +385,7 @@ __device__ __forceinline__ void zf_window(const ZfArgs& a, int64_t b, int64_t s0
     }
 }
 
-template <int FMT, int NB>
+template <int FMT, int NB, int OUT>
 __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
     // LDS: the per-wave transpose buffers, aliased by the workgroup's block sums before the slide
     constexpr int RED = ZF_WAVES * 3 * ZF_G * 17;
@@ -444,7 +448,7 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
         double ar[NB], ai[NB], br_[NB], bi[NB];
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
-            const int64_t row = (b * NB + r) * a.T;
+            const int64_t row = (b * a.nb_all + a.br0 + r) * a.T;
             double2 va = make_double2(0.0, 0.0), vb = make_double2(0.0, 0.0);
             if (lane < cnt) va = ld_c<FMT, double>(a.x, row + sg + lane);
             if (lane < cnt && sg + N + lane < a.T) vb = ld_c<FMT, double>(a.x, row + sg + N + lane);
@@ -489,8 +493,17 @@ __global__ __launch_bounds__(64 * ZF_WAVES) void zc_freq_kernel(ZfArgs a) {
                 Ci += red[1][lane][g];
                 E += red[2][lane][g];
             }
-            const double den = a.t_energy * E;
-            static_cast<double*>(a.metric)[b * a.noff + og + lane] = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
+            const int64_t o = b * a.noff + og + lane;
+            if constexpr (OUT == ZF_PART || OUT == ZF_PART_ADD) {
+                double* p = static_cast<double*>(a.metric) + 3 * o;
+                if constexpr (OUT == ZF_PART_ADD) { Cr += p[0]; Ci += p[1]; E += p[2]; }
+                p[0] = Cr; p[1] = Ci; p[2] = E;
+            } else {
+                const double den = a.t_energy * E;
+                const double m = (Cr * Cr + Ci * Ci) / (den > 1e-12 ? den : 1e-12);
+                if constexpr (OUT == ZF_F32) static_cast<float*>(a.metric)[o] = (float)m;
+                else static_cast<double*>(a.metric)[o] = m;
+            }
         }
         wave_sync();
     }
@@ -1019,16 +1032,55 @@ static bool zw_ok(int in_fmt, int precision, int N, int64_t noff) {
            (R & (R - 1)) == 0 && noff <= 64;
 }
 
-template <int FMT>
-static int zf_launch(const ZfArgs& a, int nb, hipStream_t st) {
-    const dim3 grid((unsigned)(a.B * ((a.nchunks + ZF_WAVES - 1) / ZF_WAVES)));   // a stream's chunk groups
+template <int FMT, int OUT>
+static int zf_launch_out(const ZfArgs& a, int nb, hipStream_t st) {
+    const int64_t groups = a.B * ((a.nchunks + ZF_WAVES - 1) / ZF_WAVES);     // a stream's chunk groups
+    if (groups > 0x7fffffff) return OFS_EINVAL;
+    const dim3 grid((unsigned)groups);
     switch (nb) {
-        case 1: hipLaunchKernelGGL((zc_freq_kernel<FMT, 1>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((zc_freq_kernel<FMT, 2>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((zc_freq_kernel<FMT, 3>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
-        default: hipLaunchKernelGGL((zc_freq_kernel<FMT, 4>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        case 1: hipLaunchKernelGGL((zc_freq_kernel<FMT, 1, OUT>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((zc_freq_kernel<FMT, 2, OUT>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((zc_freq_kernel<FMT, 3, OUT>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
+        default: hipLaunchKernelGGL((zc_freq_kernel<FMT, 4, OUT>), grid, dim3(64 * ZF_WAVES), 0, st, a); break;
     }
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
+}
+template <int FMT>
+static int zf_launch(const ZfArgs& a, int nb, int out, hipStream_t st) {
+    switch (out) {
+        case ZF_F32: return zf_launch_out<FMT, ZF_F32>(a, nb, st);
+        case ZF_PART: return zf_launch_out<FMT, ZF_PART>(a, nb, st);
+        case ZF_PART_ADD: return zf_launch_out<FMT, ZF_PART_ADD>(a, nb, st);
+        default: return zf_launch_out<FMT, ZF_F64>(a, nb, st);
+    }
+}
+// chunks of offsets for zc_freq_kernel: halve from ~N while the grid has fewer than 4096 chunks in
+// all (variant ZF_ITEMS overrides the target)
+static void zf_chunks(ZfArgs& a) {
+    const int64_t zfv = ofs::variant_or(ofs::V_ZF_ITEMS, 4096);
+    const int64_t zf_items = zfv > 0 ? zfv : 4096;
+    int64_t chunk = ((std::max<int64_t>(a.N, 256) + 63) / 64) * 64;
+    while (chunk > 256 && a.B * ((a.noff + chunk - 1) / chunk) < zf_items) chunk = ((chunk / 2 + 63) / 64) * 64;
+    a.chunk = chunk;
+    a.nchunks = (a.noff + chunk - 1) / chunk;
+}
+static int zf_dispatch(int in_fmt, ZfArgs& a, int nb, int out, hipStream_t st) {
+    zf_chunks(a);
+    switch (in_fmt) {
+        case OFS_C64: return zf_launch<OFS_C64>(a, nb, out, st);
+        case OFS_C128: return zf_launch<OFS_C128>(a, nb, out, st);
+        default: return zf_launch<OFS_CI16>(a, nb, out, st);
+    }
+}
+
+// metric = (C_re² + C_im²) / max(E_t·D, 1e-12) from accumulated partial sums
+template <class OUTT>
+__global__ __launch_bounds__(256) void zf_finish_kernel(const double* __restrict__ part, int64_t n, double e_t,
+                                                        OUTT* __restrict__ metric) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double cr = part[3 * i], ci = part[3 * i + 1], den = e_t * part[3 * i + 2];
+    metric[i] = (OUTT)((cr * cr + ci * ci) / (den > 1e-12 ? den : 1e-12));
 }
 
 }  // namespace
@@ -1096,6 +1148,19 @@ static bool zs_enabled() {                 // variant ZS=0: the earlier one-chun
     return !ofs::variant_off(ofs::V_ZS);
 }
 
+// template bins into the kernel argument block (reduced mod N: fftshift(fft)[(N/2+k)%N] = fft[k mod N])
+static void zf_bins(ZfArgs& a, int32_t n_bins, const int32_t* bin_indices, const double* template_bins) {
+    const int N = a.N;
+    for (int i = 0; i < 64; ++i) {
+        if (i < n_bins) {
+            a.kb[i] = (int)(((bin_indices[i] % N) + N) % N);
+            a.tr[i] = template_bins[2 * i]; a.ti[i] = template_bins[2 * i + 1];
+        } else {
+            a.kb[i] = 0; a.tr[i] = 0.0; a.ti[i] = 0.0;
+        }
+    }
+}
+
 int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T,
                            int32_t N, int32_t cp, int32_t precision, int32_t n_bins,
                            const int32_t* bin_indices, const double* template_bins,
@@ -1110,14 +1175,8 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
     ZfArgs a;
     a.x = x; a.B = B; a.T = T; a.N = N; a.cp = cp; a.noff = noff;
     a.nbins = n_bins; a.t_energy = template_energy; a.metric = metric;
-    for (int i = 0; i < 64; ++i) {
-        if (i < n_bins) {
-            a.kb[i] = (int)(((bin_indices[i] % N) + N) % N);   // fftshift(fft)[(N/2+k)%N] = fft[k mod N]
-            a.tr[i] = template_bins[2 * i]; a.ti[i] = template_bins[2 * i + 1];
-        } else {
-            a.kb[i] = 0; a.tr[i] = 0.0; a.ti[i] = 0.0;
-        }
-    }
+    a.nb_all = n_br; a.br0 = 0;
+    zf_bins(a, n_bins, bin_indices, template_bins);
     hipStream_t st = (hipStream_t)stream;
     if (precision == OFS_FP32) {
         if (zw_ok(in_fmt, precision, N, noff)) {          // few offsets per stream: window FFTs
@@ -1128,7 +1187,11 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
         // many offsets: the fp64 sliding DFT, metric rounded to fp32 (its only fp32 step)
         const int r = ofs_zc_slide_launch(in_fmt, n_br, 1, x, B, T, N, cp, n_bins, a.kb, a.tr, a.ti,
                                           template_energy, metric, st);
-        return r == 1 ? OFS_OK : (r == 0 ? OFS_EINVAL : r);
+        if (r != 0) return r == 1 ? OFS_OK : r;
+        // shapes the block-initialised kernel does not take (3-4 branches, N not a multiple of 64,
+        // blocks beyond LDS): the one-chunk-per-wave fp64 sliding DFT, metric rounded to fp32
+        if (n_br > 4) return OFS_EINVAL;
+        return zf_dispatch(in_fmt, a, n_br, ZF_F32, st);
     }
     if (zs_enabled()) {
         const int r = ofs_zc_slide_launch(in_fmt, n_br, 0, x, B, T, N, cp, n_bins, a.kb, a.tr, a.ti,
@@ -1136,18 +1199,41 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
         if (r != 0) return r == 1 ? OFS_OK : r;
     }
     if (n_br > 4) return OFS_EINVAL;
-    // chunks of offsets: halve from ~N while the grid has fewer than 4096 chunks in all (variant ZF_ITEMS)
-    const int64_t zfv = ofs::variant_or(ofs::V_ZF_ITEMS, 4096);
-    const int64_t zf_items = zfv > 0 ? zfv : 4096;
-    int64_t chunk = ((std::max<int64_t>(N, 256) + 63) / 64) * 64;
-    while (chunk > 256 && B * ((noff + chunk - 1) / chunk) < zf_items) chunk = ((chunk / 2 + 63) / 64) * 64;
-    a.chunk = chunk;
-    a.nchunks = (noff + chunk - 1) / chunk;
-    switch (in_fmt) {
-        case OFS_C64: return zf_launch<OFS_C64>(a, n_br, st);
-        case OFS_C128: return zf_launch<OFS_C128>(a, n_br, st);
-        default: return zf_launch<OFS_CI16>(a, n_br, st);
-    }
+    return zf_dispatch(in_fmt, a, n_br, ZF_F64, st);
+}
+
+int32_t ofs_zc_freq_partial(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T, int32_t br0,
+                            int32_t n_grp, int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
+                            const double* template_bins, int32_t accumulate, double* part, void* stream) {
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || OFS_MISSING(part, B) || !bin_indices || !template_bins || B < 0 ||
+        n_br < 1 || br0 < 0 || n_grp < 1 || n_grp > 4 || br0 + n_grp > n_br || T < 0 || N < 1 || cp < 0 ||
+        n_bins < 1 || n_bins > 64)
+        return OFS_EINVAL;
+    const int64_t noff = T - ((int64_t)N + cp) + 1;
+    if (noff <= 0) return OFS_ESHORT;
+    if (B == 0) return OFS_OK;
+    ZfArgs a;
+    a.x = x; a.B = B; a.T = T; a.N = N; a.cp = cp; a.noff = noff;
+    a.nbins = n_bins; a.t_energy = 1.0; a.metric = part;
+    a.nb_all = n_br; a.br0 = br0;
+    zf_bins(a, n_bins, bin_indices, template_bins);
+    return zf_dispatch(in_fmt, a, n_grp, accumulate ? ZF_PART_ADD : ZF_PART, (hipStream_t)stream);
+}
+
+int32_t ofs_zc_freq_finish(const double* part, int64_t B, int64_t noff, double template_energy, int32_t precision,
+                           void* metric, void* stream) {
+    if (B < 0 || noff < 0 || OFS_MISSING(part, B * noff) || OFS_MISSING(metric, B * noff) ||
+        !(precision == OFS_FP32 || precision == OFS_FP64))
+        return OFS_EINVAL;
+    const int64_t n = B * noff;
+    if (n == 0) return OFS_OK;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    hipStream_t st = (hipStream_t)stream;
+    if (precision == OFS_FP32)
+        hipLaunchKernelGGL(zf_finish_kernel<float>, grid, dim3(256), 0, st, part, n, template_energy, (float*)metric);
+    else
+        hipLaunchKernelGGL(zf_finish_kernel<double>, grid, dim3(256), 0, st, part, n, template_energy, (double*)metric);
+    return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
 
 int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N, int32_t cp) {
@@ -1155,7 +1241,7 @@ int32_t ofs_zc_freq_plan(int32_t in_fmt, int32_t precision, int64_t T, int32_t N
     if (noff <= 0) return 0;
     if (precision == OFS_FP32) {
         if (zw_ok(in_fmt, precision, N, noff)) return (N == 4096 && zw64_enabled()) ? 3 : 2;
-        return ofs_zc_slide_ok(in_fmt, 1, N, 62, noff) ? 5 : 0;
+        return ofs_zc_slide_ok(in_fmt, 1, N, 62, noff) ? 5 : 6;
     }
     return (zs_enabled() && ofs_zc_slide_ok(in_fmt, 1, N, 62, noff)) ? 4 : 1;
 }

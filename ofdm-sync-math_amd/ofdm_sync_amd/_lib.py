@@ -107,6 +107,9 @@ def _declare(lib):
         "ofs_sc_gate": (c_int32, [c_int32, P, c_int64, c_int64, c_double, P, P, P]),
         "ofs_segment_peak": (c_int32, [P, P, c_int64, c_int64, c_int64, c_int64, P, P, P]),
         "ofs_zc_freq_plan": (c_int32, [c_int32, c_int32, c_int64, c_int32, c_int32]),
+        "ofs_zc_freq_partial": (c_int32, [c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32, c_int32,
+                                          c_int32, c_int32, P, P, c_int32, P, P]),
+        "ofs_zc_freq_finish": (c_int32, [P, c_int64, c_int64, c_double, c_int32, P, P]),
         "ofs_zc_fft_plan_create": (c_int32, [c_int32, c_int32, c_int64, c_int64, P,
                                              ctypes.POINTER(ctypes.c_size_t)]),
         "ofs_zc_fft_plan_create2": (c_int32, [c_int32, c_int32, c_int64, c_int64, c_int32, P,

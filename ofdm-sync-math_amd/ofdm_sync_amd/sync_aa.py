@@ -246,6 +246,12 @@ def aa_detect_streaming_batched(x, L: int = PREAMBLE_HALF_LEN, threshold: float 
     Same per-stream semantics as ``aa_detect_streaming``; results stay on the GPU.
     ``precision``: None (fp64 for complex128/int16 input, fp32 for complex64), 'fp32', 'fp64'.
     ``placement``: output backing, "plain" or "contiguous" (see ``allocate``).
+
+    Detect-only calls (``outputs=()``) on the fp32 fast path run their own arithmetic (fp32 row
+    scans, 4 samples per lane; the storing call scans in fp64): their events can differ from a
+    storing call's, but only where the reference's own float64 decision is a near-tie (a metric
+    within 1e-6 of the threshold, or two |P|^2 candidates within 1e-5 relative in a gate) -
+    tests/test_gpu_detect_only.py::test_default_detect_only_vs_default_full_near_threshold.
     """
     batch = _lib.as_batch(x, batched=True)
     prec = _lib.resolve_precision(batch, precision)

@@ -39,31 +39,47 @@ def make_pss_frequency_template() -> tuple[np.ndarray, np.ndarray, float]:
     return bin_indices, template_bins, energy
 
 
+MAX_GROUP_BRANCHES = 4      # ofs_zc_freq_partial: branches per kernel pass
+MAX_GROUP_BINS = 64         # template bins per kernel pass (one lane per bin)
+
+
 def _run(batch: _lib.Batch, N: int, cp: int, bin_indices, template_bins, template_energy,
          precision=None):
-    idx = np.ascontiguousarray(np.asarray(bin_indices).astype(np.int32))
-    tb = np.ascontiguousarray(np.asarray(template_bins, dtype=np.complex128))
-    if idx.ndim != 1 or tb.shape != idx.shape:
+    idx = np.ascontiguousarray(np.asarray(bin_indices).reshape(-1).astype(np.int32))
+    tb = np.ascontiguousarray(np.asarray(template_bins, dtype=np.complex128).reshape(-1))
+    if np.asarray(bin_indices).ndim != 1 or tb.shape != idx.shape:
         raise ValueError("bin_indices and template_bins must be 1-D of equal length")
-    if idx.size > 64 or idx.size == 0:
-        raise ValueError("ofs_zc_freq_metric supports 1..64 template bins")
     noff = batch.T - (N + cp) + 1
     if noff <= 0:
         raise ValueError("Received stream is shorter than a single OFDM symbol.")
     L = _lib.lib()
     prec = _lib.resolve_precision(batch, precision)     # complex64 -> fp32 result, whatever the offsets
-    if prec == _lib.FP32 and L.ofs_zc_freq_plan(batch.fmt, _lib.FP32, batch.T, int(N), int(cp)) not in (2, 3) and (
-            batch.nb > 2 or N % 64):
-        raise ValueError("fp32 zc_freq over many offsets needs N a multiple of 64 and <= 2 receive branches "
-                         "(the sliding-DFT kernel); use precision='fp64'")
-    if prec == _lib.FP64 and batch.nb > 4:
-        raise ValueError("the fp64 zc_freq kernel supports up to 4 receive branches")
-    out = torch.empty((batch.B, noff), dtype=torch.float64 if prec == _lib.FP64 else torch.float32,
-                      device=batch.data.device)
-    rc = L.ofs_zc_freq_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, int(N),
-                              int(cp), prec, int(idx.size), idx.ctypes.data, tb.ctypes.data,
-                              float(template_energy), out.data_ptr(), _lib.stream_ptr())
-    _lib.check(rc, "ofs_zc_freq_metric")
+    dev = batch.data.device
+    out = torch.empty((batch.B, noff), dtype=torch.float64 if prec == _lib.FP64 else torch.float32, device=dev)
+    if idx.size == 0:                                   # no bins: corr 0, energy 0 -> 0 / max(0, eps)
+        return out.zero_()
+    if batch.nb <= MAX_GROUP_BRANCHES and idx.size <= MAX_GROUP_BINS:
+        rc = L.ofs_zc_freq_metric(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, int(N),
+                                  int(cp), prec, int(idx.size), idx.ctypes.data, tb.ctypes.data,
+                                  float(template_energy), out.data_ptr(), _lib.stream_ptr())
+        _lib.check(rc, "ofs_zc_freq_metric")
+        return out
+    # any branch count / template length (zc_freq.py:85-97 loops over both): partial sums of the
+    # numerator C and the energy D over groups of <= 4 branches x <= 64 bins, one normalisation
+    part = torch.empty((batch.B, noff, 3), dtype=torch.float64, device=dev)
+    first = True
+    for br0 in range(0, batch.nb, MAX_GROUP_BRANCHES):
+        ng = min(MAX_GROUP_BRANCHES, batch.nb - br0)
+        for j0 in range(0, idx.size, MAX_GROUP_BINS):
+            ig = np.ascontiguousarray(idx[j0:j0 + MAX_GROUP_BINS])
+            tg = np.ascontiguousarray(tb[j0:j0 + MAX_GROUP_BINS])
+            rc = L.ofs_zc_freq_partial(batch.fmt, batch.data.data_ptr(), batch.B, batch.nb, batch.T, br0, ng,
+                                       int(N), int(cp), int(ig.size), ig.ctypes.data, tg.ctypes.data,
+                                       0 if first else 1, part.data_ptr(), _lib.stream_ptr())
+            _lib.check(rc, "ofs_zc_freq_partial")
+            first = False
+    _lib.check(L.ofs_zc_freq_finish(part.data_ptr(), batch.B, noff, float(template_energy), prec, out.data_ptr(),
+                                    _lib.stream_ptr()), "ofs_zc_freq_finish")
     return out
 
 

@@ -526,3 +526,50 @@ def test_zc_fft_plan_shared_by_two_streams():
     torch.cuda.synchronize()
     for i, g in enumerate(got):
         assert torch.equal(g, want[i % 2])
+
+
+@pytest.mark.parametrize("fmt,nb,nbins,N,cp,T", [("c128", 6, 62, 256, 64, 1500), ("c128", 1, 100, 256, 32, 900),
+                                                 ("c64", 6, 100, 128, 16, 700), ("c64", 3, 62, 256, 64, 1500),
+                                                 ("c64", 4, 62, 200, 20, 900), ("int16", 5, 70, 192, 0, 800),
+                                                 ("c128", 9, 130, 64, 16, 300)])
+def test_zc_freq_any_branches_and_bins(fmt, nb, nbins, N, cp, T):
+    """zc_freq.py:62-99 loops over any number of branches and template bins: more than 4 branches
+    or 64 bins run as partial sums over groups of <= 4 x <= 64 (ofs_zc_freq_partial + _finish);
+    complex64 with 3-4 branches or N not a multiple of 64 over many offsets falls back to the
+    one-chunk-per-wave fp64 kernel with an fp32 metric.  Against the oracle: 1e-9 relative for fp64
+    output, fp32 rounding of the fp64 metric (2^-23 relative) for complex64."""
+    rng = np.random.default_rng(nb * 100 + nbins)
+    B = 3
+    x = rng_c(rng, B, nb, T)
+    x[1, :, 100:100 + N] += 3 * O.pss_symbol(N, length=min(62, N - 2 - (N % 2)))
+    half = nbins // 2
+    idx = np.concatenate((np.arange(-half, 0), np.arange(1, nbins - half + 1)))
+    t = np.exp(-1j * np.pi * 25 * np.arange(nbins) * (np.arange(nbins) + 1) / nbins)
+    e = float(np.sum(np.abs(t) ** 2))
+    if fmt == "int16":
+        xi = np.stack([np.round(x.real * 100), np.round(x.imag * 100)], -1).astype(np.int16)
+        xd, x = torch.from_numpy(xi).cuda(), xi[..., 0] + 1j * xi[..., 1]
+    elif fmt == "c64":
+        x = x.astype(np.complex64)
+        xd = torch.from_numpy(x).cuda()
+    else:
+        xd = torch.from_numpy(x).cuda()
+    m = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp)
+    assert m.dtype == (torch.float32 if fmt == "c64" else torch.float64)
+    m = m.cpu().numpy().astype(np.float64)
+    for b in range(B):
+        mo = O.zc_freq_metric(x[b].astype(np.complex128), N, cp, idx, t, e)
+        if fmt == "c64":
+            np.testing.assert_allclose(m[b], mo, rtol=2.0 ** -22, atol=1e-12)
+        else:
+            np.testing.assert_allclose(m[b], mo, rtol=1e-9, atol=1e-11)
+    if fmt != "c64":                       # the drop-in: numpy in, reference globals for N / cp
+        import ofdm_sync_amd.zc_freq as zf
+        old = (zf.N_FFT, zf.CYCLIC_PREFIX)
+        zf.N_FFT, zf.CYCLIC_PREFIX = N, cp
+        try:
+            m1 = zf.compute_frequency_metric(x[1], idx, t, e)
+        finally:
+            zf.N_FFT, zf.CYCLIC_PREFIX = old
+        np.testing.assert_allclose(m1, O.zc_freq_metric(x[1].astype(np.complex128), N, cp, idx, t, e),
+                                   rtol=1e-9, atol=1e-11)
