@@ -32,8 +32,9 @@ using namespace ofs;
 namespace {
 
 // streams per workgroup (walker lanes) and helper waves: LDS-DMA path 16 streams, 7 helpers (one
-// 116 KiB workgroup of 8 waves per CU); register path 8 streams, 3 helpers (its staging registers
-// scale with the stream count)
+// workgroup of 8 waves per CU; static LDS (4 + 3 + 2) x 16 x 130 doubles = 149,760 B = 146.25 KiB of
+// gfx950's 160 KiB, asserted in the kernel); register path 8 streams, 3 helpers ((3 + 2 + 2) x 8 x
+// 130 doubles = 57 KiB; its staging registers scale with the stream count)
 #ifndef OFS_ZC_S
 #define OFS_ZC_S 16
 #endif
@@ -175,6 +176,8 @@ void zc_cfar_kernel(ZcArgs a) {
     __shared__ double tc[NC][ZS][ZP];     // c
     __shared__ double to[NO][ZS][ZP];     // c[i - W] (0 before the window fills)
     __shared__ double ta[2][ZS][ZP];      // running sum after sample i
+    static_assert(sizeof(tc) + sizeof(to) + sizeof(ta) <= 160 * 1024,
+                  "zc_cfar_kernel: static LDS beyond gfx950's 160 KiB per workgroup (OFS_ZC_S / ZC / ZP)");
     const int lane = threadIdx.x & 63;
     // role of this wave: 0 = walker, 1..ZH = helpers.  (Measured and not kept: the walker chosen by
     // SIMD id so both workgroups' walkers share a SIMD, 0.38 -> 0.45 ms; an idle 8th wave as the

@@ -219,6 +219,9 @@ def receiver_backend(rx, pilot_cp_start: int, data_cp_start: int, pilot_used, da
 # drivers call them (sc.py:274-311).  Each has the reference's name, signature and return
 # convention (numpy in -> numpy out; torch in -> device tensors) and runs on the GPU; the
 # *_batched forms take [B, n] device rows.  The fused chain above stays the fast path.
+# Precision: every helper computes in fp64 and returns complex128 / float64 whatever the input
+# precision (the reference's drivers hand these helpers complex128 arrays; for complex64 input
+# numpy would compute and return complex64 - the fp64 result is the more accurate of the two).
 # ---------------------------------------------------------------------------------------------
 def _rows(a, dev, dtype=torch.complex128):
     """(device tensor [B, n] of `dtype`, was_numpy, original ndim) for 1-D or 2-D input."""
@@ -310,6 +313,10 @@ def _cdiv(y, d, eps):
     dev = _lib.require_gpu()
     t, from_numpy, nd = _rows(y, dev)
     B, n = t.shape
+    dn = d.dim() if isinstance(d, torch.Tensor) else np.ndim(d)
+    if nd == 1 and dn == 2:                  # numpy broadcasting: a [n] numerator against [B, n] rows
+        Bd = int(d.shape[0])
+        t, B, nd = t.expand(Bd, n).contiguous(), Bd, 2
     r, rs = _ref_rows(d, B, n, dev)
     out = torch.empty_like(t)
     _lib.check(_lib.lib().ofs_cdiv_eps(t.data_ptr(), B, n, r.data_ptr(), rs, float(eps), out.data_ptr(),
@@ -337,7 +344,7 @@ def remove_common_phase(x, ref=None):
     B, n = t.shape
     if n == 0:                                          # np.mean of nothing: nan
         cpe = float("nan")
-        return (x.copy() if from_numpy else x.clone()), cpe
+        return (np.array(x, dtype=np.complex128, copy=True) if from_numpy else x.clone()), cpe
     r, rs = _ref_rows(ref, B, n, dev) if ref is not None else (None, 0)
     out = torch.empty_like(t)
     cpe = torch.empty((B,), dtype=torch.float64, device=dev)

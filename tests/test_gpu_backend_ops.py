@@ -151,3 +151,21 @@ def test_run_simulation_chain_rebound_helper_by_helper(name):
     fused = core.receiver_backend(rx, ps, ds, d["pilot_used"], d["data_used"])
     close(fused["h"], h, 1e-11)
     assert abs(fused["evm"] - evm) <= 1e-10 * evm
+
+
+def test_division_broadcasts_like_numpy_and_empty_paths():
+    """A [n] numerator against [B, n] divisors broadcasts to [B, n] like numpy's Y / (X + eps);
+    remove_common_phase of an empty list returns an ndarray copy and nan; outputs are complex128
+    (the helpers compute in fp64 whatever the input precision)."""
+    rng = np.random.default_rng(8)
+    y = rng.standard_normal(40) + 1j * rng.standard_normal(40)
+    d = rng.standard_normal((3, 40)) + 1j * rng.standard_normal((3, 40))
+    h = core.ls_channel_estimate(y, d)
+    assert h.shape == (3, 40) and h.dtype == np.complex128
+    np.testing.assert_array_equal(h, y / (d + 1e-9))
+    x, cpe = core.remove_common_phase([])
+    assert isinstance(x, np.ndarray) and x.size == 0 and np.isnan(cpe)
+    h64 = core.equalize(y.astype(np.complex64), d[0].astype(np.complex64))
+    assert h64.dtype == np.complex128
+    np.testing.assert_allclose(h64, y.astype(np.complex64).astype(np.complex128) /
+                               (d[0].astype(np.complex64).astype(np.complex128) + 1e-9), rtol=1e-15)
