@@ -112,6 +112,32 @@ constexpr int MF_LDS = (MF_M + MF_M / 16 + 128) * 16;     // padded block + the 
 __device__ __forceinline__ double2 mf_mul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
+// w · e^{-i·pi·e8/4} for an eighth-turn count e8 in 0..3 known at compile time: the twiddles of one
+// radix group differ from its base twiddle by such exact constants, so a group reads ONE table
+// entry pair instead of one per butterfly (exponent (k + q·h)·M/(2·sp·h) = base^{R/(2sp)} · e^{-i·pi·q/sp})
+__device__ __forceinline__ double2 mf_rot8(double2 w, int e8) {
+    constexpr double r = 0.70710678118654752440;
+    switch (e8) {
+        case 0: return w;
+        case 1: return make_double2(r * (w.x + w.y), r * (w.y - w.x));
+        case 2: return make_double2(w.y, -w.x);
+        default: return make_double2(r * (w.y - w.x), -r * (w.x + w.y));
+    }
+}
+// the stage twiddle of butterfly q at half-span sp (in units of h) of a radix-R group whose powers of
+// the base twiddle are pw[0] = b, pw[1] = b^2, pw[2] = b^4
+template <int R>
+__device__ __forceinline__ double2 mf_stw(const double2 (&pw)[3], int sp, int q) {
+    const int pi = (R / (2 * sp)) == 1 ? 0 : ((R / (2 * sp)) == 2 ? 1 : 2);
+    return mf_rot8(pw[pi], q * (4 / sp));
+}
+template <int R>
+__device__ __forceinline__ void mf_powers(const double2* twq, int e, double2 (&pw)[3]) {
+    pw[0] = mf_tw(twq, e);
+    pw[1] = mf_mul(pw[0], pw[0]);
+    if (R == 8) pw[2] = mf_mul(pw[1], pw[1]);
+    else pw[2] = pw[1];
+}
 __device__ __forceinline__ void mf_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -127,12 +153,13 @@ __device__ __forceinline__ void mf_dif(double2* fb, const double2* twq, int h, c
         double2 v[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) v[i] = fb[mf_at(p + i * h)];
+        double2 pw[3];
+        mf_powers<R>(twq, k * (MF_M / (R * h)), pw);
 #pragma unroll
         for (int sp = R / 2; sp >= 1; sp >>= 1) {
-            const int str = MF_M / (2 * sp * h);
             double2 w[R / 2];
 #pragma unroll
-            for (int q = 0; q < sp; ++q) w[q] = mf_tw(twq, (k + q * h) * str);
+            for (int q = 0; q < sp; ++q) w[q] = mf_stw<R>(pw, sp, q);
 #pragma unroll
             for (int i0 = 0; i0 < R; i0 += 2 * sp)
 #pragma unroll
@@ -162,12 +189,13 @@ __device__ __forceinline__ void mf_dit(double2* fb, const double2* twq, int h) {
         double2 v[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) v[i] = fb[mf_at(p + i * h)];
+        double2 pw[3];
+        mf_powers<R>(twq, k * (MF_M / (R * h)), pw);
 #pragma unroll
         for (int sp = 1; sp < R; sp <<= 1) {
-            const int str = MF_M / (2 * sp * h);
             double2 w[R / 2];
 #pragma unroll
-            for (int q = 0; q < sp; ++q) w[q] = mf_tw(twq, (k + q * h) * str);
+            for (int q = 0; q < sp; ++q) w[q] = mf_stw<R>(pw, sp, q);
 #pragma unroll
             for (int i0 = 0; i0 < R; i0 += 2 * sp)
 #pragma unroll
@@ -204,12 +232,15 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
         const int64_t g = g0 + t + MF_T * m;
         v[m] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, row * a.T + g) : make_double2(0.0, 0.0);
     }
-    // forward DIF, spans 4096, 2048, 1024 (twiddle exponents offset·M/(2·span))
+    // forward DIF, spans 4096, 2048, 1024 (twiddle exponents offset·M/(2·span)): with b = w^t,
+    // w^{t + 1024m} = b·e^{-i pi m/4}, w^{2(t + 1024r)} = b^2·e^{-i pi r/2}, w^{4t} = b^4
+    double2 tp[3];
+    mf_powers<8>(twq, t, tp);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         const double2 x0 = v[m], x1 = v[m + 4];
         v[m] = make_double2(x0.x + x1.x, x0.y + x1.y);
-        v[m + 4] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, t + MF_T * m));
+        v[m + 4] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_rot8(tp[0], m));
     }
 #pragma unroll
     for (int m = 0; m < 8; m += 4)
@@ -217,13 +248,13 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
         for (int r = 0; r < 2; ++r) {
             const double2 x0 = v[m + r], x1 = v[m + r + 2];
             v[m + r] = make_double2(x0.x + x1.x, x0.y + x1.y);
-            v[m + r + 2] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, 2 * (t + MF_T * r)));
+            v[m + r + 2] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_rot8(tp[1], 2 * r));
         }
 #pragma unroll
     for (int m = 0; m < 8; m += 2) {
         const double2 x0 = v[m], x1 = v[m + 1];
         v[m] = make_double2(x0.x + x1.x, x0.y + x1.y);
-        v[m + 1] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), mf_tw(twq, 4 * t));
+        v[m + 1] = mf_mul(make_double2(x0.x - x1.x, x0.y - x1.y), tp[2]);
     }
 #pragma unroll
     for (int m = 0; m < 8; ++m) fb[mf_at(t + MF_T * m)] = v[m];
@@ -240,7 +271,7 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     for (int m = 0; m < 8; ++m) v[m] = fb[mf_at(t + MF_T * m)];
 #pragma unroll
     for (int m = 0; m < 8; m += 2) {                                 // span 1024
-        const double2 tt = mf_mul(mf_tw(twq, 4 * t), v[m + 1]), u = v[m];
+        const double2 tt = mf_mul(tp[2], v[m + 1]), u = v[m];
         v[m] = make_double2(u.x + tt.x, u.y + tt.y);
         v[m + 1] = make_double2(u.x - tt.x, u.y - tt.y);
     }
@@ -248,13 +279,13 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     for (int m = 0; m < 8; m += 4)                                   // span 2048
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            const double2 tt = mf_mul(mf_tw(twq, 2 * (t + MF_T * r)), v[m + r + 2]), u = v[m + r];
+            const double2 tt = mf_mul(mf_rot8(tp[1], 2 * r), v[m + r + 2]), u = v[m + r];
             v[m + r] = make_double2(u.x + tt.x, u.y + tt.y);
             v[m + r + 2] = make_double2(u.x - tt.x, u.y - tt.y);
         }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {                                    // span 4096
-        const double2 tt = mf_mul(mf_tw(twq, t + MF_T * m), v[m + 4]), u = v[m];
+        const double2 tt = mf_mul(mf_rot8(tp[0], m), v[m + 4]), u = v[m];
         v[m] = make_double2(u.x + tt.x, u.y + tt.y);
         v[m + 4] = make_double2(u.x - tt.x, u.y - tt.y);
     }

@@ -188,8 +188,8 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     batch = _lib.as_batch(x, batched=True)
     dev = batch.data.device
     r_host = _ref_host(reference)
-    ref, energy = _ref_dev(reference, r_host, dev)
-    N = int(ref.numel())
+    energy = float(np.sum(np.abs(r_host) ** 2))         # as the reference computes it (zc_v2.py:263)
+    N = int(r_host.size)
     nout = batch.T + N - 1
     shape = (batch.B, batch.nb, nout) if mode == OFS_ZC_RAW else (batch.B, nout)
     corr = torch.empty(shape, dtype=torch.complex128, device=dev) if want_corr else None
@@ -206,6 +206,7 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
         if method == "fft":
             raise RuntimeError(f"ofs_zc_mf_plan_create: no overlap-save plan for {batch.nb} branches x "
                                f"{N} taps (extract LDS); use method='direct' (status -2)")
+    ref, _ = _ref_dev(reference, r_host, dev)          # the direct sums read the taps on the device
     ci = None
     if mode == OFS_ZC_NORMALIZE:
         ci = torch.as_tensor(corr_in).to(device=dev, dtype=torch.complex128).reshape(batch.B, nout).contiguous()
