@@ -183,6 +183,20 @@ def cpu_baseline(det, L: int, threads: int, budget: float):
                               sample=f"{n1} streams x {T} c64 x{reps1} (first streams of the same batch), "
                                      f"the same C port on one thread, {dt1:.2f} s wall")
     out["per_core_Msamples_s"] = out["single_core"]["value"]
+    # every core the process may run on (one worker per core), beside the per-GPU share
+    n_all = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if n_all > threads:
+        oracle_c.aa_detect(xh[:n_all], L, nthreads=n_all)                # warm the larger pool
+        reps_a, dt_a = 0, 0.0
+        while dt_a < min(budget, 2.0) and reps_a < 50:
+            t0 = time.perf_counter()
+            oracle_c.aa_detect(xh, L, nthreads=n_all, max_events=det.max_events, want_arrays=False)
+            dt_a += time.perf_counter() - t0
+            reps_a += 1
+        out["all_cores"] = dict(value=reps_a * B * T / dt_a / 1e6, unit="Msamples/s", cores=n_all, kind="port",
+                                sample=f"full per-GPU batch x{reps_a}: {B} streams x {T} c64, the same C port with "
+                                       f"OpenMP over streams on every CPU of the process's affinity ({n_all} threads; "
+                                       f"the box's other GPUs' shares included), {dt_a:.2f} s wall")
     out["numpy"] = _pool_leg(xh, L, "numpy", threads, budget)
     out["literal_loop"] = _pool_leg(xh, L, "loop", threads, budget)
     out["other_configs"] = other_config_baselines(threads, budget)

@@ -873,7 +873,8 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(BW), lds, st, a);
         return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
     };
-    const bool fast = !ofs::variant_off(ofs::V_BE_FAST) &&    // variant BE_FAST=0: the generic kernel (A/B) (n_br == 1 || n_br == 2) && cp_len <= 2 * BW &&
+    // variant BE_FAST=0: the generic kernel (A/B)
+    const bool fast = !ofs::variant_off(ofs::V_BE_FAST) && (n_br == 1 || n_br == 2) && cp_len <= 2 * BW &&
                       ((n_fft == 4 * BW && n_used <= 3 * BW) || (n_fft == 8 * BW && n_used <= 5 * BW) ||
                        (n_fft == 16 * BW && n_used <= 10 * BW));
     if (fast) {

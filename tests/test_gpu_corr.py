@@ -325,7 +325,8 @@ def test_zc_freq_fp32_lane_reduce_kernel(B, nb, cp, T, variant):
 def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
     """complex64 input always returns float32: > 64 offsets per stream run the fp64 sliding DFT
     with the metric rounded to fp32 (plan 5), within u·m of the fp64 kernel's result; shapes the
-    sliding kernel does not take (3 branches over many offsets) raise instead of switching."""
+    block-initialised kernel does not take (3 branches over many offsets) run the one-chunk-per-wave
+    fp64 kernel, still with a float32 result (no silent dtype switch, no ValueError)."""
     from ofdm_sync_amd import _lib
     rng = np.random.default_rng(71)
     x = rng_c(rng, 3, 2, 5000).astype(np.complex64)
@@ -342,9 +343,17 @@ def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
     st = oracle_c.zc_freq_check(x, 2048, 0, idx, t, e, m.cpu().numpy(), 1e-12, 1.5)
     print(f"fp32 many offsets: max |dm| {st[:, 0].max():.3g}, max |dm|/bound {st[:, 1].max():.3g}")
     assert st[:, 1].max() <= 1.0 and mm[1].max() > 0.5
-    with pytest.raises(ValueError):                # 3 branches x many offsets: no fp32 kernel
-        zc_freq.compute_frequency_metric_batched(torch.zeros((1, 3, 5000), dtype=torch.complex64, device="cuda"),
-                                                 idx, t, e, N=2048, cp=0, precision="fp32")
+    # 3 branches x many offsets: not a shape of the block-initialised kernel; the one-chunk-per-wave
+    # fp64 kernel takes it with the metric rounded to fp32 (plan 6 for one branch is the same path)
+    x3 = rng_c(rng, 2, 3, 3000).astype(np.complex64)
+    x3[0, :, 500:500 + 2048] += 3 * O.pss_symbol(2048)
+    m3 = zc_freq.compute_frequency_metric_batched(torch.from_numpy(x3).cuda(), idx, t, e, N=2048, cp=0,
+                                                  precision="fp32")
+    assert m3.dtype == torch.float32
+    for b in range(2):
+        mo = O.zc_freq_metric(x3[b].astype(np.complex128), 2048, 0, idx, t, e)
+        np.testing.assert_allclose(m3[b].cpu().numpy().astype(np.float64), mo, rtol=2.0 ** -22, atol=1e-12)
+    assert _lib.lib().ofs_zc_freq_plan(_lib.C64, _lib.FP32, 5000, 2000, 0) == 6        # N % 64 != 0
 
 
 @pytest.mark.parametrize("fmt,N,cp,T,nb", [("c128", 2048, 512, 16384, 1), ("c128", 2048, 512, 4242, 2),

@@ -71,7 +71,7 @@ def test_default_detect_only_vs_default_full_near_threshold():
     within 1e-5 relative)."""
     import oracle_c
     import parity
-    B, T, L, thr = 4096, 1024, 512, 0.15
+    B, T, L, thr = 4096, 1024, 256, 0.15
     rng = np.random.default_rng(2024)
     a = (rng.choice([-1.0, 1.0], (B, L)) + 1j * rng.choice([-1.0, 1.0], (B, L))) / np.sqrt(2)
     snr = 10 ** (rng.uniform(-3.2, -0.8, B) / 10)

@@ -419,8 +419,9 @@ def cfg3_pcie(dev, st, steps, warmup):
 
 
 def _aa_cfg(dev, st, steps, warmup, name, B, na, T, L, dtype, prec, workload, seed):
-    """sync_aa detector on a [B, na, T] batch through the product's AABatchDetector (plain
-    placement), P/R/M + events; algorithmic bytes = input + P/R/M per time index."""
+    """sync_aa detector on a [B, na, T] batch through the product's AABatchDetector (its default
+    placement="auto", the placement used is recorded), P/R/M + events; algorithmic bytes = input +
+    P/R/M per time index."""
     from ofdm_sync_amd import sync_aa
     det = sync_aa.AABatchDetector(B, T, na, L, precision=prec, in_dtype=dtype, outputs=("P", "R", "M"),
                                   max_events=4, device=dev)
@@ -433,7 +434,8 @@ def _aa_cfg(dev, st, steps, warmup, name, B, na, T, L, dtype, prec, workload, se
     stored = int(torch.clamp(det.result.n_events, max=4).sum().item())
     kern = {10: "aa_fast_kernel (register-staged)", 11: "aa_stream_kernel (streaming)",
             30: "aa_exact_kernel<C128> (fp64 wave per stream)"}.get(plan // 100, "general engine")
-    return dict(config=name, workload=workload, kernel=f"{kern}, plan {plan}", samples=B * na * T, ms=ms,
+    return dict(config=name, workload=workload, kernel=f"{kern}, plan {plan}", placement=det.placement,
+                samples=B * na * T, ms=ms,
                 alg_bytes=B * T * (na * esz + osz) + B * 4 + stored * 64,
                 bytes_per_sample=f"{na} x {esz} in + P/R/M {osz} per time index + events")
 
@@ -503,21 +505,34 @@ def zc_mf(dev, st, steps, warmup, method="fft"):
         if best is None or nblk_m * m < best:
             best, M = nblk_m * m, m
     nblk = -(-nout // (M - N + 1))
-    spec = B * nblk * M * 16
-    traffic = (B * T * 16 + spec) + 2 * spec + 2 * spec + 2 * spec + (B * nout * 16 + B * T * 16 + B * nout * 24)
+    fused = method == "fft" and M == 8192 and _lib.get_variant("MC_FUSED") != 0
+    if fused:
+        # one LDS kernel per block (zc_fftcorr.hip mc_fused_kernel, extract fused for one branch): x read
+        # once per block (M samples incl. the N-1 overlap), corr + |corr| written once; no scratch
+        traffic = B * nblk * M * 16 + B * nout * 24
+        model = "x read once per block (M = 8192 incl. the N-1 overlap) + corr 16 B + |corr| 8 B out"
+        kern = "mc_fused_kernel<C128, fused extract>: load + DIF FFT + xH/M + DIT inverse + normalise in LDS"
+    else:
+        spec = B * nblk * M * 16
+        traffic = (B * T * 16 + spec) + 2 * spec + 2 * spec + 2 * spec + (B * nout * 16 + B * T * 16 + B * nout * 24)
+        model = ("pack (x in, spectra out) + rocFFT fwd (r+w) + xH (r+w) + rocFFT inv (r+w) + extract "
+                 "(valid spectra + x for the energy prefix in, corr + |corr| out)")
+        kern = "FFT overlap-save: pack + rocFFT fwd + xH + rocFFT inv + extract/normalise (fp64)"
     r = dict(config="zc_mf" if method == "fft" else "zc_mf_direct",
              workload=f"zc_v2 matched filter + normalise, N={N} taps, {B} x {T} c128, fp64",
-             kernel=("FFT overlap-save: pack + rocFFT fwd + xH + rocFFT inv + extract/normalise (fp64)"
-                     if method == "fft" else "zc_mf_kernel<fp64> (direct correlation, LDS tile)"),
+             kernel=kern if method == "fft" else "zc_mf_kernel<fp64> (direct correlation, LDS tile)",
              samples=B * T, ms=ms, alg_bytes=B * T * 16 + B * nout * 24,
              bytes_per_sample="16 in + corr 16 + |corr| 8 out")
     if method == "fft":
-        r.update(fft_block=M, fft_blocks=nblk, traffic_model_bytes=traffic,
-                 traffic_model="pack (x in, spectra out) + rocFFT fwd (r+w) + xH (r+w) + rocFFT inv (r+w) + extract "
-                               "(valid spectra + x for the energy prefix in, corr + |corr| out)",
-                 traffic_frac=round(traffic / (ms / 1e3) / 1e9 / HBM, 4))
-    # the direct-sum work (8N flops per output) is the reference's algorithm; the FFT path does far
-    # less arithmetic, so its flop_frac is quoted against the direct count ("direct-equivalent")
+        # the FFT path's own work: per block two M-point complex FFTs (5·M·log2 M flops each), the
+        # pointwise product with H/M (6 flops per point) and the normalisation (~10 per output)
+        fft_flops = B * nblk * (2 * 5 * M * (M.bit_length() - 1) + 6 * M) + B * nout * 10
+        r.update(fft_block=M, fft_blocks=nblk, traffic_model_bytes=traffic, traffic_model=model,
+                 traffic_frac=round(traffic / (ms / 1e3) / 1e9 / HBM, 4),
+                 direct_equivalent_flops=B * nout * (8 * N + 4),
+                 direct_equivalent_tflops=round(B * nout * (8 * N + 4) / (ms / 1e3) / 1e12, 2))
+        return _flops(r, fft_flops, "fp64")
+    # the direct sums: 8N flops per output (the reference's algorithm) + the |x|^2 window
     return _flops(r, B * nout * (8 * N + 4), "fp64")
 
 
