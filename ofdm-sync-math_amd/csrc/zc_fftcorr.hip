@@ -97,6 +97,9 @@ __global__ __launch_bounds__(FW) void mc_mul_kernel(double2* U, const double2* H
 // the scratch the extract kernel reads.  512 x 16384 c128, 2048 taps: pack + rocFFT + multiply +
 // rocFFT (~305 us) -> 160-173 us; the whole matched filter 0.52 -> 0.37 ms (profiles/r03z*).
 constexpr int MF_T = 1024;
+#ifndef OFS_MC_MID16
+#define OFS_MC_MID16 1          // the transforms' middle (spans 8..1, xH, 1..8) as one 16-element pass
+#endif
 constexpr int MF_M = 8 * MF_T;
 
 // twiddle w^e, e < M/2, from two 64-entry LDS tables: w^e = w^{64·(e>>6)} · w^{e & 63} (one complex
@@ -211,6 +214,81 @@ __device__ __forceinline__ void mf_dit(double2* fb, const double2* twq, int h) {
     mf_sync();
 }
 
+// v · e^{-i·pi·q/8}, q in 0..7 known at compile time (the 16th roots of unity of a radix-16 group at
+// offset k = 0, whose twiddles are all constants)
+__device__ __forceinline__ double2 mf_w16(double2 v, int q) {
+    constexpr double c = 0.92387953251128675613, s = 0.38268343236508977173, r = 0.70710678118654752440;
+    switch (q) {
+        case 0: return v;
+        case 1: return make_double2(v.x * c + v.y * s, v.y * c - v.x * s);
+        case 2: return make_double2(r * (v.x + v.y), r * (v.y - v.x));
+        case 3: return make_double2(v.x * s + v.y * c, v.y * s - v.x * c);
+        case 4: return make_double2(v.y, -v.x);
+        case 5: return make_double2(v.y * c - v.x * s, -(v.y * s + v.x * c));
+        case 6: return make_double2(r * (v.y - v.x), -r * (v.x + v.y));
+        default: return make_double2(v.y * s - v.x * c, -(v.y * c + v.x * s));
+    }
+}
+// The middle of the matched filter in ONE LDS pass: the forward transform's last four DIF stages
+// (spans 8, 4, 2, 1), the product with H/M in bit-reversed order and the conjugation, then the
+// inverse's first four DIT stages (spans 1, 2, 4, 8) all act on the same 16 contiguous elements.  A
+// lane pair holds one such group (lane t: elements 8t .. 8t+7, its partner t^1 the other half); the
+// span-8 stages pair element i with i + 8 across the pair (DPP quad_perm [1,0,3,2] swap), spans 4..1
+// stay inside a lane.  Every twiddle is a 16th root of unity (offset k = 0 in the group): constants.
+// 1 LDS pass and barrier instead of 4, all 1024 threads busy.
+__device__ __forceinline__ double2 mf_swap_pair(double2 v) {
+    return make_double2(ofs::dpp_d<0xB1>(v.x), ofs::dpp_d<0xB1>(v.y));
+}
+__device__ __forceinline__ void mf_mid16(double2* fb, const double2* __restrict__ Hbr) {
+    const int t = threadIdx.x;
+    const bool hi = (t & 1) != 0;                   // elements 8..15 of the group
+    double2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = fb[mf_at(8 * t + i)];
+    // DIF span 8: a = element i, b = element i + 8 -> a + b (low half), (a - b)·w16^i (high half)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double2 o = mf_swap_pair(v[i]);
+        const double2 a = hi ? o : v[i], b = hi ? v[i] : o;
+        v[i] = hi ? mf_w16(make_double2(a.x - b.x, a.y - b.y), i) : make_double2(a.x + b.x, a.y + b.y);
+    }
+#pragma unroll
+    for (int sp = 4; sp >= 1; sp >>= 1)
+#pragma unroll
+        for (int i0 = 0; i0 < 8; i0 += 2 * sp)
+#pragma unroll
+            for (int q = 0; q < sp; ++q) {
+                const double2 a = v[i0 + q], b = v[i0 + q + sp];
+                v[i0 + q] = make_double2(a.x + b.x, a.y + b.y);
+                v[i0 + q + sp] = mf_w16(make_double2(a.x - b.x, a.y - b.y), q * (8 / sp));
+            }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double2 y = mf_mul(v[i], Hbr[8 * t + i]);
+        v[i] = make_double2(y.x, -y.y);
+    }
+#pragma unroll
+    for (int sp = 1; sp <= 4; sp <<= 1)
+#pragma unroll
+        for (int i0 = 0; i0 < 8; i0 += 2 * sp)
+#pragma unroll
+            for (int q = 0; q < sp; ++q) {
+                const double2 tt = mf_w16(v[i0 + q + sp], q * (8 / sp)), u = v[i0 + q];
+                v[i0 + q] = make_double2(u.x + tt.x, u.y + tt.y);
+                v[i0 + q + sp] = make_double2(u.x - tt.x, u.y - tt.y);
+            }
+    // DIT span 8: u = element i, w = w16^i · element i + 8 -> u + w (low half), u - w (high half)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double2 o = mf_swap_pair(v[i]);
+        const double2 u = hi ? o : v[i], w = mf_w16(hi ? v[i] : o, i);
+        v[i] = hi ? make_double2(u.x - w.x, u.y - w.y) : make_double2(u.x + w.x, u.y + w.y);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fb[mf_at(8 * t + i)] = v[i];
+    mf_sync();
+}
+
 template <int FMT, bool FUSE_X>
 __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2* __restrict__ Hbr) {
     extern __shared__ __attribute__((aligned(16))) double2 fb[];     // [MF_M + pads], then 2 x 64 twiddles
@@ -261,14 +339,19 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     mf_sync();
     mf_dif<8, false>(fb, twq, 128, Hbr);                             // spans 512, 256, 128
     mf_dif<8, false>(fb, twq, 16, Hbr);                              // 64, 32, 16
+#if OFS_MC_MID16
+    mf_mid16(fb, Hbr);                                               // 8, 4, 2, 1; conj(X·H/M); 1, 2, 4, 8
+#else
     mf_dif<4, false>(fb, twq, 4, Hbr);                               // 8, 4
     mf_dif<4, true>(fb, twq, 1, Hbr);                                // 2, 1; then conj(X·H/M)
     mf_dit<4>(fb, twq, 1);                                           // spans 1, 2
     mf_dit<4>(fb, twq, 4);                                           // 4, 8
+#endif
     mf_dit<8>(fb, twq, 16);                                          // 16, 32, 64
     mf_dit<8>(fb, twq, 128);                                         // 128, 256, 512
 #pragma unroll
     for (int m = 0; m < 8; ++m) v[m] = fb[mf_at(t + MF_T * m)];
+    mf_powers<8>(twq, t, tp);            // recomputed here rather than held across the LDS passes
 #pragma unroll
     for (int m = 0; m < 8; m += 2) {                                 // span 1024
         const double2 tt = mf_mul(tp[2], v[m + 1]), u = v[m];

@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.."
 f=${1:-corr}
 out=/tmp/ru_$f.txt
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -c ofdm-sync-math_amd/csrc/$f.hip \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude ${RU_FLAGS} -c ofdm-sync-math_amd/csrc/$f.hip \
   -o /tmp/ru_$f.o -Rpass-analysis=kernel-resource-usage > $out 2>&1
 rc=$?
 grep -E "error" $out | head -20
