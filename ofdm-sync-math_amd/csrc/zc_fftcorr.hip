@@ -36,7 +36,7 @@ struct McPlan {
     int32_t N = 0, M = 0, S = 0, nb = 0;
     int64_t B = 0, T = 0, nblk = 0, nout = 0;
     double2* H = nullptr;           // [M] FFT of the reversed conjugated reference
-    double2* Hbr = nullptr;         // fused path (M = MF_M): H[bitrev(i)] / M
+    double2* Hbr = nullptr;         // fused path (M = MF_M): H[bitrev(i)] / M, then 128 twiddles
     double ref_norm = 0.0;
     size_t work_bytes = 0;
     size_t scratch_bytes = 0;
@@ -111,6 +111,8 @@ __device__ __forceinline__ double2 mf_tw(const double2* tws, int e) {
 // LDS position of block element e: one 16-byte pad per 16 elements, so the radix passes with small
 // spans (elements 4 or 16 apart in consecutive lanes) spread over the banks
 __device__ __forceinline__ int mf_at(int e) { return e + (e >> 4); }
+// LDS position of the energy prefix P[j], j <= M (fused extract): eight planes of 1025 doubles
+__device__ __forceinline__ int mf_pq(int j) { return (j & 7) * 1025 + (j >> 3); }
 constexpr int MF_LDS = (MF_M + MF_M / 16 + 128) * 16;     // padded block + the two twiddle tables
 __device__ __forceinline__ double2 mf_mul(double2 a, double2 b) {
     return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -294,11 +296,7 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     extern __shared__ __attribute__((aligned(16))) double2 fb[];     // [MF_M + pads], then 2 x 64 twiddles
     const int t = threadIdx.x;
     double2* tws = fb + MF_M + MF_M / 16;
-    if (t < 128) {                                                    // w^l, l < 64; w^{64h}, h < 64
-        double sn, cs;
-        sincospi(-2.0 * (double)(t < 64 ? t : 64 * (t - 64)) / (double)MF_M, &sn, &cs);
-        tws[t] = make_double2(cs, sn);
-    }
+    if (t < 128) tws[t] = Hbr[MF_M + t];                              // w^l, l < 64; w^{64h}, h < 64 (plan)
     mf_sync();
     const double2* twq = tws;
     const int64_t blk = blockIdx.x;                                   // row·nblk + q
@@ -385,8 +383,12 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     // window energies from an fp64 prefix of |u_q|^2 over the block, in the (now free) block LDS:
     // thread t scans u[8t .. 8t+7] (re-read, L2), block scan of the thread totals, P[j] = Σ_{i<j}
     mf_sync();
-    double* P = reinterpret_cast<double*>(fb);                      // [MF_M + 1] (+ per-wave totals)
-    double* wt = P + MF_M + 1;
+    // P[j] lives at mf_pq(j) = (j & 7)·1025 + (j >> 3): thread t's eight consecutive prefixes go to eight
+    // planes at the same column t (consecutive lanes, consecutive words), and the reads P[o + 1],
+    // P[o + 1 - N] of consecutive o hit different planes (bank offset 2·(j & 7) + 2·(j >> 3)); the plain
+    // layout [8t + i] put every 4th lane on one bank (16-way conflicts on the prefix stores)
+    double* P = reinterpret_cast<double*>(fb);                      // 8 x 1025 (+ per-wave totals)
+    double* wt = P + 8 * 1025;
     double e8[8], loc = 0.0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -407,9 +409,9 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     mf_sync();
     double run = incl - loc;
     for (int k = 0; k < wv; ++k) run += wt[k];
-    if (t == 0) P[0] = 0.0;
+    if (t == 0) P[mf_pq(0)] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { run += e8[i]; P[8 * t + i + 1] = run; }
+    for (int i = 0; i < 8; ++i) { run += e8[i]; P[mf_pq(8 * t + i + 1)] = run; }
     mf_sync();
     const int64_t n0 = q * a.S;
     const int ns = (int)min((int64_t)a.S, a.nout - n0);
@@ -419,28 +421,35 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
         if (s < 0 || s >= ns) continue;
         const double2 c = make_double2(v[m].x, -v[m].y);
         const int64_t oi = row * a.nout + n0 + s;                    // one branch: row = stream
+        // |.| as sqrt(re² + im²) and the normalisation as one reciprocal and two products: within an
+        // ulp or two of numpy's hypot and true division (the block FFT's own error is ~1e-14 of the
+        // row), without hypot's scaling branches and two fp64 divisions per output
         if (a.mode == OFS_ZC_RAW || a.mode == OFS_ZC_SUM) {
             if (a.out) a.out[oi] = c;
-            if (a.mag) a.mag[oi] = hypot(c.x, c.y);
+            if (a.mag) a.mag[oi] = sqrt(fma(c.x, c.x, c.y * c.y));
             continue;
         }
-        const double e = P[o + 1] - P[o + 1 - a.N];                  // Σ |x|^2 over the N-sample window
-        double2 r;
-        if (a.mode == OFS_ZC_V2) {
-            const double d = a.ref_norm * sqrt(e > 1e-12 ? e : 1e-12);
-            r = make_double2(c.x / d, c.y / d);
-        } else {                                                     // OFS_ZC_COMBINED
-            const double d = a.ref_norm * sqrt((e > 0.0 ? e : 0.0) + 1e-12);
-            r = make_double2(c.x / d, c.y / d);
-        }
+        const double e = P[mf_pq(o + 1)] - P[mf_pq(o + 1 - a.N)];  // Σ |x|^2 over the N-sample window
+        const double ew = a.mode == OFS_ZC_V2 ? (e > 1e-12 ? e : 1e-12)                 // zc_v2.py:268
+                                              : (e > 0.0 ? e : 0.0) + 1e-12;            // zc.py:113-126
+        const double inv = 1.0 / (a.ref_norm * sqrt(ew));
+        const double2 r = make_double2(c.x * inv, c.y * inv);
         if (a.out) a.out[oi] = r;
-        if (a.mag) a.mag[oi] = hypot(r.x, r.y);
+        if (a.mag) a.mag[oi] = sqrt(fma(r.x, r.x, r.y * r.y));
     }
 }
 
-// Hbr[i] = H[bitrev(i)] / M, for the fused path
+// Hbr[i] = H[bitrev(i)] / M, for the fused path; then the kernel's two 64-entry twiddle tables
+// Hbr[M + l] = w^l, Hbr[M + 64 + h] = w^{64h} (from sincospi of exact ratios, once per plan)
 __global__ void mc_prep_kernel(const double2* H, double2* Hbr, int M, int lb) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M; i += gridDim.x * blockDim.x) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < M + 128; i += gridDim.x * blockDim.x) {
+        if (i >= M) {
+            const int l = i - M;
+            double sn, cs;
+            sincospi(-2.0 * (double)(l < 64 ? l : 64 * (l - 64)) / (double)M, &sn, &cs);
+            Hbr[i] = make_double2(cs, sn);
+            continue;
+        }
         const int r = (int)(__brev((unsigned)i) >> (32 - lb));
         const double2 h = H[r];
         Hbr[i] = make_double2(h.x / (double)M, h.y / (double)M);
@@ -633,8 +642,8 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
     const size_t lds = extract_lds(p->nb, p->M);
     bool ok2 = rocfft_execution_info_create(&p->info) == rocfft_status_success;
     if (ok2 && p->M == MF_M) {                  // fused path resources (optional: rocFFT otherwise)
-        if (hipMalloc(&p->Hbr, (size_t)MF_M * sizeof(double2)) == hipSuccess) {
-            hipLaunchKernelGGL(mc_prep_kernel, dim3(MF_M / 256), dim3(256), 0, 0, p->H, p->Hbr, MF_M, 13);
+        if (hipMalloc(&p->Hbr, (size_t)(MF_M + 128) * sizeof(double2)) == hipSuccess) {
+            hipLaunchKernelGGL(mc_prep_kernel, dim3(MF_M / 256 + 1), dim3(256), 0, 0, p->H, p->Hbr, MF_M, 13);
             const size_t fl = MF_LDS;
             const bool okf = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
                 hipFuncSetAttribute((const void*)mc_fused_kernel<OFS_C64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fl) == hipSuccess &&

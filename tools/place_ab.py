@@ -22,6 +22,10 @@ SHAPES = {                       # name: (B, n_ant, T, L, cir branches)
     "cfg3_2ant": (65536, 2, 1024, 512, (0, 1)),
     "cfg3_T4096": (65536, 1, 4096, 512, (1,)),
     "aa_refshape_c64": (16384, 2, 5315, 512, (0, 1)),
+    "aa_1ant_T5315": (16384, 1, 5315, 512, (1,)),
+    "aa_2ant_T4096": (16384, 2, 4096, 512, (0, 1)),
+    "aa_2ant_T5316": (16384, 2, 5316, 512, (0, 1)),
+    "aa_1ant_T4095": (65536, 1, 4095, 512, (1,)),
 }
 
 
