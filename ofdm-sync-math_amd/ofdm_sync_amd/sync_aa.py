@@ -167,11 +167,14 @@ class AABatchDetector:
     stream produced more (its count stays exact in ``n_events``; the batched function re-runs
     in that case, this class leaves it to the caller).
 
-    ``placement="auto"`` (default) backs the buffers the way measured fastest for the precision:
-    fp32 (complex64 in) every buffer its own physically contiguous block (headline cfg3 0.27-0.30
-    vs 0.30-0.33 ms plain; two antennas -1.5 %), fp64 one plain arena (cfg3 in fp64: contiguous
-    0.99 vs 0.59 ms; cfg2a 0.044 vs 0.030 ms); when the driver cannot back a
-    contiguous block it falls back to "plain".  ``self.placement`` is the placement used.
+    ``placement="auto"`` (default) backs the buffers the way measured fastest for the shape: fp32
+    (complex64 in) with whole 8 KiB stream rows (T a multiple of 1024) every buffer its own physically
+    contiguous block, everything else one plain arena.  Paired A/B, fresh detectors per round
+    (tools/place_ab.py, profiles/r04b_placement_ab.jsonl, r04c_placement_ab.jsonl; contiguous / plain):
+    cfg3 0.96, two antennas 0.98, T = 4096 0.88, 2 x 4096 0.99 - but the reference's own 2 x 5315
+    shape 1.16, 2 x 5316 1.30, 1 x 4095 1.02 (1 x 5315 0.95 is the one row-unaligned shape it helps);
+    fp64 contiguous 0.99 vs 0.59 ms (cfg3), cfg2a 0.044 vs 0.030 ms.  When the driver
+    cannot back a contiguous block it falls back to "plain".  ``self.placement`` is the placement used.
     """
 
     def __init__(self, B: int, T: int, n_ant: int = 1, L: int = PREAMBLE_HALF_LEN,
@@ -195,7 +198,8 @@ class AABatchDetector:
             want = tuple(set(want) | {"P", "M"})         # tiled general engine: events from P/M in HBM
         specs = [(xshape, in_dtype), ((B, T), ct) if "P" in want else None, ((B, T), rt) if "R" in want else None,
                  ((B, T), rt) if "M" in want else None, ((B, T), torch.bool) if "valid" in want else None]
-        used = placement if placement != "auto" else ("contiguous" if prec == _lib.FP32 else "plain")
+        used = placement if placement != "auto" else (
+            "contiguous" if prec == _lib.FP32 and T % 1024 == 0 else "plain")
         try:
             self.x, P, R, M, V = allocate(dev, specs, used)
         except MemoryError:
