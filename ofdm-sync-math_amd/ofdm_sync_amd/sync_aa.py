@@ -143,9 +143,10 @@ def _run(batch: _lib.Batch, L: int, threshold: float, hysteresis: int, sample_ra
                                 ((B, T), torch.bool) if "valid" in want else None], placement)
     n_ev = ev_i = ev_r = None
     if detect:
-        # every stream's count is written by the kernel; event slots past it are not, and are
-        # left uninitialised (no per-call memset of 2 x B x E x 32 B; readers mask with live_events)
-        n_ev = torch.empty((B,), dtype=torch.int32, device=dev)
+        # counts zeroed (4 B per stream: T = 0 launches nothing); event slots past a stream's count
+        # are never written and stay uninitialised (no per-call memset of 2 x B x E x 32 B; readers
+        # mask with live_events)
+        n_ev = torch.zeros((B,), dtype=torch.int32, device=dev)
         ev_i = torch.empty((B, max(max_events, 1), 4), dtype=torch.int64, device=dev)
         ev_r = torch.empty((B, max(max_events, 1), 4), dtype=torch.float64, device=dev)
     rc = _lib.lib().ofs_aa_detect(batch.fmt, batch.data.data_ptr(), B, batch.nb, T, int(L), prec,
