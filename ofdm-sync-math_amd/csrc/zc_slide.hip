@@ -99,6 +99,14 @@ constexpr int ZS_G = 16;               // steps per group (one d staging, one st
 __host__ __device__ constexpr int zs_stg(int C, int rows) {
     return C > ZS_G * rows ? (C > 128 ? C : 128) : (ZS_G * rows > 128 ? ZS_G * rows : 128);
 }
+// pair kernel: per-wave staging = one branch's block staging, or phase 2's d values of every branch
+__host__ __device__ constexpr int zs_pair_stgw(int C, int rows, int nb) {
+    return zs_stg(C, rows) > nb * rows * ZS_G ? zs_stg(C, rows) : nb * rows * ZS_G;
+}
+// pair kernel LDS: one branch's blocks (the workgroup's chunks + N/C - 1) + the waves' staging
+__host__ __device__ constexpr size_t zs_pair_lds(int C, int N, int rows, int W, int nb) {
+    return ((size_t)(rows * W + N / C - 1) * 64 + (size_t)W * zs_pair_stgw(C, rows, nb)) * 16;
+}
 constexpr int ZS_RG = 4;               // DEFER: steps per LDS partial round
 constexpr int ZS_PS = 3 * 64 + 2;      // DEFER: doubles per step plane [cr, ci, e][64 lanes] + 16 B, so the
                                        // four summing lanes of a row read different bank groups
@@ -113,7 +121,7 @@ constexpr int ZS_PS = 3 * 64 + 2;      // DEFER: doubles per step plane [cr, ci,
 // nblk blocks into beta[m][NB][64 slots], one block per wave at a time (lane = bin slot, Horner in
 // w^{4k} over four interleaved chains, samples broadcast from the wave's LDS staging).
 template <int FMT, int NB>
-__device__ __forceinline__ void zs_blocks(const ZsArgs& a, double2* beta, double2* stg, int STG, int64_t b, int64_t c0,
+__device__ __forceinline__ void zs_blocks(const ZsArgs& a, double2* beta, double2* stg, int STG, int64_t row0, int64_t c0,
                                           int nblk, int lane, int w) {
     const int C = a.C, N = a.N, W = a.W;
     const int kb = lane < a.nbins ? a.kb[lane] : 0;
@@ -125,7 +133,7 @@ __device__ __forceinline__ void zs_blocks(const ZsArgs& a, double2* beta, double
         for (int r = 0; r < NB; ++r)
             for (int j = lane; j < C; j += 64) {
                 const int64_t i = s0 + j;
-                stg[r * STG + j] = i < a.T ? ldx<FMT>(a.x, (b * NB + r) * a.T + i) : make_double2(0.0, 0.0);
+                stg[r * STG + j] = i < a.T ? ldx<FMT>(a.x, (row0 + r) * a.T + i) : make_double2(0.0, 0.0);
             }
         wave_sync();
 #pragma unroll
@@ -155,7 +163,7 @@ __device__ __forceinline__ void zs_blocks(const ZsArgs& a, double2* beta, double
 // (the resonator's state grows at most ~M²·|x| at φ -> 0, so the error stays ~M²·2^-53 relative).
 // Samples are staged 64 per block at a time, so the staging area is the per-bin kernel's.
 template <int FMT, int NB>
-__device__ __forceinline__ void zs_blocks_pair(const ZsArgs& a, double2* beta, double2* stg, int STG, int64_t b,
+__device__ __forceinline__ void zs_blocks_pair(const ZsArgs& a, double2* beta, double2* stg, int STG, int64_t row0,
                                                int64_t c0, int nblk, int lane, int w) {
     const int C = a.C, N = a.N, W = a.W, M = C / 4;
     const int half = lane >> 5, p = lane & 31;
@@ -176,7 +184,7 @@ __device__ __forceinline__ void zs_blocks_pair(const ZsArgs& a, double2* beta, d
             for (int r = 0; r < NB; ++r)
                 for (int j = lane; j < 128; j += 64) {
                     const int64_t i = a.cp + (c0 + m0 + (j >> 6)) * (int64_t)C + hb + (j & 63);
-                    stg[r * STG + j] = i < a.T ? ldx<FMT>(a.x, (b * NB + r) * a.T + i) : make_double2(0.0, 0.0);
+                    stg[r * STG + j] = i < a.T ? ldx<FMT>(a.x, (row0 + r) * a.T + i) : make_double2(0.0, 0.0);
                 }
             wave_sync();
 #pragma unroll
@@ -252,7 +260,7 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_slide_kernel(ZsArgs a) {
     double2* stg = zsm + (size_t)(BPL * W + NQ - 1) * NB * 64 + (size_t)w * NB * STG;   // per wave [NB][STG]
 
     // ---- phase 1: block DFTs (lane = bin slot) ----
-    zs_blocks<FMT, NB>(a, beta, stg, STG, b, c0, nblk, lane, w);
+    zs_blocks<FMT, NB>(a, beta, stg, STG, b * NB, c0, nblk, lane, w);
     __syncthreads();
 
     // ---- phase 2: BPL chunks per wave, BPL bins per lane ----
@@ -439,23 +447,54 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
     const int64_t c0 = gi * ROWS * (int64_t)W;
     const int64_t c1 = min(c0 + ROWS * (int64_t)W, a.nchunks);
     const int nblk = (int)(c1 - c0) + NQ - 1;
-    double2* beta = zsm;                                               // [nblk][NB][64]
-    double2* stg = zsm + (size_t)(ROWS * W + NQ - 1) * NB * 64 + (size_t)w * NB * STG;
-    if (a.gblk)
-        zs_blocks_pair<FMT, NB>(a, beta, stg, STG, b, c0, nblk, lane, w);
-    else
-        zs_blocks<FMT, NB>(a, beta, stg, STG, b, c0, nblk, lane, w);
-    __syncthreads();
+    // Blocks of ONE branch at a time (NBB = 1 row of 64 slots per block): the branch's initial windows
+    // are built from them before the next branch's blocks overwrite the region, so the workgroup's LDS
+    // holds one branch's blocks (two branches: half the LDS, twice the resident workgroups)
+    constexpr int NBB = 1;
+    double2* beta = zsm;                                               // [nblk][NBB][64]
+    double2* stg = zsm + (size_t)(ROWS * W + NQ - 1) * NBB * 64 + (size_t)w * zs_pair_stgw(C, ROWS, NB);
 
     const int row = lane / LPC, sl = lane % LPC;
     const int64_t c = c0 + ROWS * (int64_t)w + row;
     const bool idle = c0 + ROWS * (int64_t)w >= c1;
-    if (!DEFER && idle) return;
     const bool live = c < c1;
     const int cl = live ? (int)(c - c0) : 0;
-    double c2[PPL], dm[PPL];
-    double2 A[PPL], Bc[PPL], g[PPL][NB], h[PPL][NB];
+    double2 g[PPL][NB], h[PPL][NB];
     double epp = 0.0;                                                  // Σ |h|² (last step's Σ |g|²)
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+        if (rb > 0) __syncthreads();                                   // the previous branch's blocks are read
+        if (a.gblk)
+            zs_blocks_pair<FMT, NBB>(a, beta, stg, zs_stg(C, ROWS), b * NB + rb, c0, nblk, lane, w);
+        else
+            zs_blocks<FMT, NBB>(a, beta, stg, zs_stg(C, ROWS), b * NB + rb, c0, nblk, lane, w);
+        __syncthreads();
+        // branch rb's initial windows: X_s[±k] = Σ_{q<N/C} w^{±kqC} β_{±k}(c + q)
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) {
+            const int p = sl + LPC * q;
+            const bool valid = p < a.npairs && !idle;
+            const int k = valid ? a.pk[p] : 1, sp = valid ? a.ps[p] : 0, sn = valid ? a.pn[p] : 0;
+            const double2 w1 = twid(k, N);
+            const double inv2s = -0.5 / w1.y;                          // 1 / (2 sin θ)
+            const double2 step = twid(((int64_t)k * C) % N, N);        // w^{kC}
+            double2 t = make_double2(1.0, 0.0), xp = make_double2(0.0, 0.0), xn = make_double2(0.0, 0.0);
+            for (int pq = 0; pq < (valid ? NQ : 0); ++pq) {
+                xp = cfma(t, beta[(cl + pq) * NBB * 64 + sp], xp);
+                xn = cfma(make_double2(t.x, -t.y), beta[(cl + pq) * NBB * 64 + sn], xn);
+                t = cmul(t, step);
+            }
+            const double2 yp = cmul(w1, xp), yn = cmul(make_double2(w1.x, -w1.y), xn);
+            const double2 hh = make_double2((yp.y - yn.y) * inv2s, -(yp.x - yn.x) * inv2s);   // -i(y+ - y-)/(2 sin θ)
+            const double2 gg = cfma(w1, hh, yp);
+            h[q][rb] = valid ? hh : make_double2(0.0, 0.0);
+            g[q][rb] = valid ? gg : make_double2(0.0, 0.0);
+            epp = fma(h[q][rb].x, h[q][rb].x, fma(h[q][rb].y, h[q][rb].y, epp));
+        }
+    }
+    if (!DEFER && idle) return;                                        // (no barrier follows)
+    double c2[PPL], dm[PPL];
+    double2 A[PPL], Bc[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; ++q) {
         const int p = sl + LPC * q;
@@ -468,28 +507,6 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
         Bc[q] = valid ? make_double2(-(tp.x + tn.x), -(tp.y + tn.y)) : make_double2(0.0, 0.0);
         c2[q] = valid ? 2.0 * w1.x : 0.0;
         dm[q] = valid ? 1.0 : 0.0;
-        const double inv2s = -0.5 / w1.y;                              // 1 / (2 sin θ)
-        const double2 step = twid(((int64_t)k * C) % N, N);            // w^{kC}
-        double2 t = make_double2(1.0, 0.0), xp[NB], xn[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) { xp[r] = make_double2(0.0, 0.0); xn[r] = make_double2(0.0, 0.0); }
-        for (int pq = 0; pq < (valid ? NQ : 0); ++pq) {
-#pragma unroll
-            for (int r = 0; r < NB; ++r) {
-                xp[r] = cfma(t, beta[((cl + pq) * NB + r) * 64 + sp], xp[r]);
-                xn[r] = cfma(make_double2(t.x, -t.y), beta[((cl + pq) * NB + r) * 64 + sn], xn[r]);
-            }
-            t = cmul(t, step);
-        }
-#pragma unroll
-        for (int r = 0; r < NB; ++r) {
-            const double2 yp = cmul(w1, xp[r]), yn = cmul(make_double2(w1.x, -w1.y), xn[r]);
-            const double2 hh = make_double2((yp.y - yn.y) * inv2s, -(yp.x - yn.x) * inv2s);   // -i(y+ - y-)/(2 sin θ)
-            const double2 gg = cfma(w1, hh, yp);
-            h[q][r] = valid ? hh : make_double2(0.0, 0.0);
-            g[q][r] = valid ? gg : make_double2(0.0, 0.0);
-            epp = fma(h[q][r].x, h[q][r].x, fma(h[q][r].y, h[q][r].y, epp));
-        }
     }
     double2* dbuf = stg;                                               // [NB][ROWS][ZS_G]
     const int64_t o0 = c * (int64_t)C;
@@ -747,6 +764,7 @@ extern "C" int ofs_zc_slide_launch(int fmt, int n_br, int out_f32, const void* x
     a.npairs = 0;
     a.gblk = !ofs::variant_off(ofs::V_ZS_GBLK);                     // 0: Horner block DFTs in the pair kernel (A/B)
     const bool pair = zs_pair_enabled() && bpl == (n_br == 2 ? 4 : 8) && zs_pairs(a);
+    if (pair) lds = zs_pair_lds(a.C, N, bpl, a.W, n_br);        // one branch's blocks at a time
 #define ZS_CASE(F, NBV) \
     if (fmt == F && n_br == NBV) \
         return f ? zs_go<F, NBV, float>(a, lds, bpl, pair, st) : zs_go<F, NBV, double>(a, lds, bpl, pair, st);
