@@ -117,6 +117,21 @@ def _cpu_share() -> int:
     return min(n, env) if env > 0 else n
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup's quota allows (cgroup v2 cpu.max 'quota period', v1 cfs files), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return None
+
+
 def _pool_leg(xh, L, form, workers, budget):
     sys_dir = os.path.join(ROOT, "oracle")
     with tempfile.TemporaryDirectory() as d:
@@ -183,8 +198,17 @@ def cpu_baseline(det, L: int, threads: int, budget: float):
                               sample=f"{n1} streams x {T} c64 x{reps1} (first streams of the same batch), "
                                      f"the same C port on one thread, {dt1:.2f} s wall")
     out["per_core_Msamples_s"] = out["single_core"]["value"]
-    # every core the process may run on (one worker per core), beside the per-GPU share
-    n_all = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    # every core the process may run on (one worker per core), beside the per-GPU share:
+    # the affinity, capped by the cgroup's CPU quota (cpu.max) - threads beyond the quota only queue
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cgroup_cpus()
+    n_all = min(n_aff, quota) if quota else n_aff
+    out["host"]["cgroup_cpu_quota"] = quota
+    out["host"]["loadavg_1m"] = round(os.getloadavg()[0], 2) if hasattr(os, "getloadavg") else None
+    if n_all <= threads:
+        out["all_cores"] = dict(value=out["value"], unit="Msamples/s", cores=threads, kind="port",
+                                sample=f"the per-GPU leg above already uses every CPU this process may run "
+                                       f"(affinity {n_aff}, cgroup quota {quota})")
     if n_all > threads:
         oracle_c.aa_detect(xh[:n_all], L, nthreads=n_all)                # warm the larger pool
         reps_a, dt_a = 0, 0.0
