@@ -35,6 +35,7 @@ from ofdm_sync_amd import _lib, shard, synth, zc_freq  # noqa: E402
 HBM = 8000.0
 VPEAK = {"fp32": 157.3, "fp64": 78.6}    # MI355X vector FMA peaks, TFLOP/s (spec; no MFMA: no contraction)
 _DIST = None                     # torch.distributed when run with N ranks (barrier before timing)
+_LAST_HOST_MS = None             # host time per step of the last timed() (enqueue only; > ms = host-bound)
 
 
 def timed(step, steps, warmup, stream):
@@ -44,10 +45,13 @@ def timed(step, steps, warmup, stream):
     if _DIST is not None:
         _DIST.barrier()
         torch.cuda.synchronize()
+    global _LAST_HOST_MS
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
+    t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    _LAST_HOST_MS = (time.perf_counter() - t0) * 1e3 / steps      # host time to enqueue one step
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / steps
@@ -690,6 +694,8 @@ def main(argv=None):
         else:
             r.update(scaling="per-rank", n_gpus=info.world)
         r["ms"] = ms
+        if _LAST_HOST_MS is not None:
+            r["host_ms_per_step"] = round(_LAST_HOST_MS, 4)
         gbs = r["alg_bytes"] / (ms / 1e3) / 1e9
         if "alg_flops" in r:
             tf = r["alg_flops"] / (ms / 1e3) / 1e12
