@@ -26,6 +26,7 @@ def main():
                                              "library reads per launch as debug variants (e.g. 'ZS_PAIR=0;ZS_PAIR=1'); "
                                              "medians of --reps")
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--prec", default="fp64", choices=("fp64", "fp32"), help="metric precision (fp32: float out)")
     a = ap.parse_args()
     dt = torch.complex128 if a.fmt == "c128" else torch.complex64
     idx, tb, e = zc_freq.make_pss_frequency_template()
@@ -33,14 +34,14 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(B)
         x = torch.randn((B, a.nb, a.T), dtype=dt, device="cuda", generator=g)
         for _ in range(3):
-            zc_freq.compute_frequency_metric_batched(x, idx, tb, e, N=a.N, cp=a.cp, precision="fp64")
+            zc_freq.compute_frequency_metric_batched(x, idx, tb, e, N=a.N, cp=a.cp, precision=a.prec)
         torch.cuda.synchronize()
 
         def run():
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()
             for _ in range(a.steps):
-                zc_freq.compute_frequency_metric_batched(x, idx, tb, e, N=a.N, cp=a.cp, precision="fp64")
+                zc_freq.compute_frequency_metric_batched(x, idx, tb, e, N=a.N, cp=a.cp, precision=a.prec)
             t1.record()
             torch.cuda.synchronize()
             return t0.elapsed_time(t1) / a.steps
