@@ -644,8 +644,10 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default=",".join(CONFIGS))
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5, help="untimed calls first (sub-ms kernels need a few "
+                                                          "to reach steady clocks: zc_freq_refshape 0.76 "
+                                                          "ms on the first timed pass vs 0.63 steady)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--cfg4-global", type=int, default=262144, help="cfg4 streams over all GPUs")
     ap.add_argument("--cfg5-global", type=int, default=1 << 20, help="cfg5 sequences over all GPUs")
