@@ -148,6 +148,21 @@ struct RowPrefix {
     }
 };
 
+// The same row prefix on int32 values (integer-valued products of 12-bit words: a row of 64·E
+// samples of one or two branches stays below 2^31), exactly the doubles' values
+template <int E>
+struct RowPrefixI {
+    int f[E], excl, tot;
+    __device__ __forceinline__ void run(const int (&v)[E]) {
+        f[0] = v[0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) f[e] = f[e - 1] + v[e];
+        const int incl = scan_add_i32(f[E - 1]);
+        excl = dppz_i<0x138>(incl);                   // wave_shr:1, lane 0 <- 0
+        tot = __builtin_amdgcn_readlane(incl, 63);
+    }
+};
+
 // ------------------------------------------------------------------------------------------
 // sync_aa, integer input (FMT = OFS_CI16, exact) or complex128 (OFS_C128, any T: stream-wide fp64
 // prefix differences, the reference's running-sum error regime; see ofs_aa_exact_plan).  P[n] = A(n) - A(n-L), R[n] = Ae(n) - Ae(n-L) with A the prefix of
@@ -436,6 +451,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
     const double keep = 1.0 - inv;
     const double scale = (double)(1ll << a.frac_bits);
     double CC = 0.0, CE = 0.0;
+    bool wide = false;                                             // a word beyond 12 bits seen (sticky)
     double sm = 0.0;                                               // IIR state carried between segments
     long long si = 0;
 #if OFS_RTL_ROUNDS_DEBUG
@@ -492,30 +508,76 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #pragma unroll
                     for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
             if (k + PD < nrows) load_row((int64_t)RL * (k + PD) + E * lane, nx[PD - 1]);
-            double pc[E], en[E];
+            // Products and energies of 12-bit words are integers below 2^23 per sample and branch: for
+            // <= 2 branches a row's prefix stays below 2^31 (2 x 2^23 x 64·E), so while every word seen
+            // so far is 12-bit (sticky, wave-uniform check; int16 input may carry wider words) the row
+            // scans run in int32 (one DPP add per step instead of three instructions per fp64 step):
+            // the same integer values exactly.
+            constexpr bool IROW = NBM <= 2 && 64 * E * NBM <= 128;
+            if constexpr (IROW && CPNA == 0) {
+                int bad = 0;
 #pragma unroll
-            for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
-#pragma unroll
-            for (int t = 0; t < NBM; ++t) {
-                if (t < nb_) {
+                for (int t = 0; t < NBM; ++t)
 #pragma unroll
                     for (int e = 0; e < E; ++e) {
-                        const int32_t d = hx(t, xsl, e);
-                        const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
-                        pc[e] += w_re(d) * xr + w_im(d) * xi;            // minn_rtl.py:616, exact
-                        en[e] += xr * xr + xi * xi;                       // :617
-                        hx(t, xsl, e) = cur[t][e];
+                        const int32_t w = cur[t][e];
+                        bad |= (int)((unsigned)((int16_t)(w & 0xffff) + 2048) >= 4096u) |
+                               (int)((unsigned)((w >> 16) + 2048) >= 4096u);
+                    }
+                wide = wide || __ballot(bad) != 0;
+            }
+            double qcf[E], qef[E], qcx, qex, qct, qet;
+            if (IROW && !wide) {
+                int pc[E], en[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) { pc[e] = 0; en[e] = 0; }
+#pragma unroll
+                for (int t = 0; t < NBM; ++t) {
+                    if (t < nb_) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int32_t d = hx(t, xsl, e);
+                            const int xr = (int16_t)(cur[t][e] & 0xffff), xi = cur[t][e] >> 16;
+                            pc[e] += (int16_t)(d & 0xffff) * xr + (d >> 16) * xi;   // minn_rtl.py:616, exact
+                            en[e] += xr * xr + xi * xi;                               // :617
+                            hx(t, xsl, e) = cur[t][e];
+                        }
                     }
                 }
+                RowPrefixI<E> ic, ie;
+                ic.run(pc); ie.run(en);
+#pragma unroll
+                for (int e = 0; e < E; ++e) { qcf[e] = (double)ic.f[e]; qef[e] = (double)ie.f[e]; }
+                qcx = (double)ic.excl; qex = (double)ie.excl; qct = (double)ic.tot; qet = (double)ie.tot;
+            } else {
+                double pc[E], en[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) { pc[e] = 0.0; en[e] = 0.0; }
+#pragma unroll
+                for (int t = 0; t < NBM; ++t) {
+                    if (t < nb_) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const int32_t d = hx(t, xsl, e);
+                            const double xr = w_re(cur[t][e]), xi = w_im(cur[t][e]);
+                            pc[e] += w_re(d) * xr + w_im(d) * xi;            // minn_rtl.py:616, exact
+                            en[e] += xr * xr + xi * xi;                       // :617
+                            hx(t, xsl, e) = cur[t][e];
+                        }
+                    }
+                }
+                RowPrefix<E> dc, de;
+                dc.run(pc); de.run(en);
+#pragma unroll
+                for (int e = 0; e < E; ++e) { qcf[e] = dc.f[e]; qef[e] = de.f[e]; }
+                qcx = dc.excl; qex = de.excl; qct = dc.tot; qet = de.tot;
             }
-            RowPrefix<E> qc, qe;
-            qc.run(pc); qe.run(en);
             const int s0r = k % NR;                                        // slot of row k
             const int s1 = (k + NR - MW) % NR, s2 = (k + NR - 2 * MW) % NR, s3 = (k + NR - 3 * MW) % NR;
 #pragma unroll
             for (int e = 0; e < E; ++e) {
-                const double c0 = (CC + qc.excl) + qc.f[e];
-                const double e0 = (CE + qe.excl) + qe.f[e];
+                const double c0 = (CC + qcx) + qcf[e];
+                const double e0 = (CE + qex) + qef[e];
                 hac(s0r, e) = c0;
                 hae(s0r, e) = e0;
                 // prefixes before the stream start are 0
@@ -546,7 +608,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                     if (a.mvalid) a.mvalid[gi] = (uint8_t)(i >= vstart);
                 }
             }
-            CC += qc.tot; CE += qe.tot;
+            CC += qct; CE += qet;
         }
         if (!seq) continue;
         const int64_t c0 = s0 + (int64_t)SC * lane;                   // first sample of my chunk

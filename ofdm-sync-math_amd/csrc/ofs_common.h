@@ -187,6 +187,21 @@ __device__ __forceinline__ double scan_add(double v) {
 }
 __device__ __forceinline__ double shr1z(double v) { return dppz<0x138>(v); }   // wave_shr:1, lane 0 <- 0
 
+// the same ladder on 32-bit integers (one v_add with a DPP source per step; exact)
+template <int CTRL, int RMASK = 0xf>
+__device__ __forceinline__ int dppz_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, RMASK, 0xf, true);
+}
+__device__ __forceinline__ int scan_add_i32(int v) {
+    v += dppz_i<0x111>(v);
+    v += dppz_i<0x112>(v);
+    v += dppz_i<0x114>(v);
+    v += dppz_i<0x118>(v);
+    v += dppz_i<0x142, 0xa>(v);
+    v += dppz_i<0x143, 0xc>(v);
+    return v;
+}
+
 // the same ladder on floats (one v_add_f32 with a DPP source per step)
 template <int CTRL, int RMASK = 0xf>
 __device__ __forceinline__ float dppz_f(float v) {
