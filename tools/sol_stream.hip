@@ -149,6 +149,19 @@ __global__ void write4(float4* __restrict__ a, int64_t n4) {
         a[i] = make_float4(1.f, 2.f, 3.f, (float)i);
 }
 
+// cfg2b (minn_rtl int12) byte mix: 4 B in, six f64 arrays + two u8 arrays out (50 B) per sample;
+// a thread handles 2 consecutive samples (16-byte stores per f64 array)
+__global__ void pattern_cfg2b(const int2* __restrict__ x, double2* o0, double2* o1, double2* o2, double2* o3,
+                              double2* o4, double2* o5, uchar2* f0, uchar2* f1, int64_t n2) {
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n2; q += (int64_t)gridDim.x * blockDim.x) {
+        const int2 w = x[q];
+        const double a = (double)w.x, b = (double)w.y;
+        o0[q] = make_double2(a, b); o1[q] = make_double2(b, a); o2[q] = make_double2(a + 1, b);
+        o3[q] = make_double2(a, b + 1); o4[q] = make_double2(a * 2, b); o5[q] = make_double2(a, b * 2);
+        f0[q] = make_uchar2((unsigned char)w.x, (unsigned char)w.y); f1[q] = make_uchar2(1, (unsigned char)q);
+    }
+}
+
 template <class F>
 static double time_ms(F f, int iters) {
     hipEvent_t e0, e1;
@@ -230,6 +243,22 @@ int main(int argc, char** argv) {
         report("write4 grid=full", 1.0 * n * 8,
                time_ms([&] { write4<<<(unsigned)((n * 8 / 16 + 255) / 256), 256>>>(P1b, n * 8 / 16); }, iters));
         CK(hipFree(P2)); CK(hipFree(R2)); CK(hipFree(M2)); CK(hipFree(P1b)); CK(hipFree(R1b)); CK(hipFree(M1b));
+    }
+    {   // cfg2b mix at this B (4096 = the cfg2b batch): 4 B in, 50 B out per sample
+        double2* o[6];
+        uchar2 *f0, *f1;
+        for (auto& p : o) CK(hipMalloc(&p, n * 8));
+        CK(hipMalloc(&f0, n)); CK(hipMalloc(&f1, n));
+        for (int grid_mult : {4, 8, 16}) {
+            snprintf(nm, sizeof nm, "pattern_cfg2b(4r+50w) grid=%dxCU", grid_mult);
+            report(nm, 54.0 * n, time_ms([&] { pattern_cfg2b<<<cus * grid_mult, 256>>>((const int2*)x, o[0], o[1], o[2], o[3],
+                                                                                          o[4], o[5], f0, f1, n / 2); }, iters));
+        }
+        report("pattern_cfg2b(4r+50w) grid=full", 54.0 * n,
+               time_ms([&] { pattern_cfg2b<<<(unsigned)((n / 2 + 255) / 256), 256>>>((const int2*)x, o[0], o[1], o[2], o[3],
+                                                                                     o[4], o[5], f0, f1, n / 2); }, iters));
+        for (auto& p : o) CK(hipFree(p));
+        CK(hipFree(f0)); CK(hipFree(f1));
     }
     report("pattern_wave(8r+16w) wave-per-stream again", 24.0 * n,
            time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
