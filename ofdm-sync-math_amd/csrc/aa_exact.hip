@@ -574,6 +574,36 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             }
             const int s0r = k % NR;                                        // slot of row k
             const int s1 = (k + NR - MW) % NR, s2 = (k + NR - 2 * MW) % NR, s3 = (k + NR - 3 * MW) % NR;
+            // steady rows (every lag row exists, every sample past the fill phase and inside the stream:
+            // wave-uniform): no availability selects, no store guards - the same values
+            if (k >= 3 * MW && (int64_t)RL * (k + 1) <= T) {
+                const bool w_cp = a.corr_positive != nullptr, w_es = a.energy_scaled != nullptr, w_mv = a.mvalid != nullptr;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const double c0 = (CC + qcx) + qcf[e];
+                    const double e0 = (CE + qex) + qef[e];
+                    hac(s0r, e) = c0;
+                    hae(s0r, e) = e0;
+                    const double c1 = hac(s1, e), c2 = hac(s2, e);
+                    const double e1 = hae(s1, e), e2 = hae(s2, e), e3 = hae(s3, e);
+                    const double ct = 0.0 + ((c0 - c1) + (c1 - c2));       // minn_rtl.py:696
+                    const double et = 0.0 + (((e0 - e1) + (e1 - e2)) + (e2 - e3));   // :697-701
+                    const double cpos = ct > 0.0 ? ct : 0.0;               // :704
+                    const double es = (a.thr_value == 0.0) ? 0.0 : et * a.thr_value;   // :718-721
+                    const int i = nb + e;
+                    const int li = (int)(i - s0);
+                    hcp[seg_at(li)] = cpos;
+                    hes[seg_at(li)] = es;
+                    const int64_t gi = row_off + i;
+                    a.corr_total[gi] = ct;
+                    if (w_cp) a.corr_positive[gi] = cpos;
+                    a.energy_total[gi] = et;
+                    if (w_es) a.energy_scaled[gi] = es;
+                    if (w_mv) a.mvalid[gi] = (uint8_t)(i >= vstart);
+                }
+                CC += qct; CE += qet;
+                continue;
+            }
 #pragma unroll
             for (int e = 0; e < E; ++e) {
                 const double c0 = (CC + qcx) + qcf[e];
