@@ -355,6 +355,16 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     mf_dit<8>(fb, twq, 128);                                         // 128, 256, 512
 #pragma unroll
     for (int m = 0; m < 8; ++m) v[m] = fb[mf_at(t + MF_T * m)];
+    // fused extract: the samples of the energy prefix (u[8t .. 8t+7], L2-resident) are requested now,
+    // so their latency hides behind the inverse's last three register stages
+    double2 u8[FUSE_X ? 8 : 1];
+    if constexpr (FUSE_X) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t g = g0 + 8 * t + i;
+            u8[i] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, row * a.T + g) : make_double2(0.0, 0.0);
+        }
+    }
     mf_powers<8>(twq, t, tp);            // recomputed here rather than held across the LDS passes
 #pragma unroll
     for (int m = 0; m < 8; m += 2) {                                 // span 1024
@@ -396,9 +406,7 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     double e8[8], loc = 0.0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const int64_t g = g0 + 8 * t + i;
-        double e = 0.0;
-        if (g >= 0 && g < a.T) { const double2 u = ldx<FMT>(a.x, row * a.T + g); e = u.x * u.x + u.y * u.y; }
+        const double e = u8[i].x * u8[i].x + u8[i].y * u8[i].y;     // 0 outside the stream (zero-filled)
         e8[i] = e;
         loc += e;
     }
