@@ -99,6 +99,17 @@ def test_argument_validation_without_gpu(lib):
                             None, None, 1, 2, 0, 4, None, None, None, None) == 0
     assert lib.ofs_cp_cfo(0, None, 0, 1, 16, None, 8, 4, 1.0, None, None, None) == 0
     assert lib.ofs_trailing_average(1, None, 0, 100, 8, 0, None, None) == 0
+    # zc_freq partial sums: branch group outside the branch count, > 4 branches or > 64 bins per group,
+    # null output; the finish kernel: bad precision; a too-short stream is OFS_ESHORT (-4)
+    ib = (ctypes.c_int32 * 2)(1, -1)
+    tb = (ctypes.c_double * 4)(1.0, 0.0, 1.0, 0.0)
+    assert lib.ofs_zc_freq_partial(0, 1, 1, 2, 100, 1, 2, 16, 0, 2, ib, tb, 0, 1, None) == -1
+    assert lib.ofs_zc_freq_partial(0, 1, 1, 6, 100, 0, 5, 16, 0, 2, ib, tb, 0, 1, None) == -1
+    assert lib.ofs_zc_freq_partial(0, 1, 1, 1, 100, 0, 1, 16, 0, 65, ib, tb, 0, 1, None) == -1
+    assert lib.ofs_zc_freq_partial(0, 1, 1, 1, 100, 0, 1, 16, 0, 2, ib, tb, 0, None, None) == -1
+    assert lib.ofs_zc_freq_partial(0, 1, 1, 1, 10, 0, 1, 16, 0, 2, ib, tb, 0, 1, None) == -4
+    assert lib.ofs_zc_freq_finish(1, 1, 10, 1.0, 7, 1, None) == -1
+    assert lib.ofs_zc_freq_finish(None, 0, 10, 1.0, 0, None, None) == 0
     # a null pointer for a NON-empty buffer is still refused
     assert lib.ofs_aa_detect(0, None, 1, 1, 1024, 512, 0, None, None, None, None, 0, 0.15, 128, 15.36e6, 0,
                              None, None, None, None) == -1
