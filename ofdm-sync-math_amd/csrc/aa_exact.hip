@@ -462,10 +462,16 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
         gate.init(a.hyst, Q, 0.0, 0.0, a.max_ev, a.ev ? a.ev + b * (int64_t)a.max_ev * 4 : nullptr,
                   nullptr, a.toff);
 
-    // rows stream in PD rows ahead of use (register queue shifted by one row per step)
-    constexpr int PD = E == 1 ? 8 : (E == 2 ? 4 : 2);
+    // Rows arrive one segment ahead of use: segment g+1's RPS rows are loaded when segment g takes its
+    // own.  gfx9 counts loads and stores on one counter (vmcnt) and they complete out of order, so the
+    // first use of a loaded register waits for EVERY memory operation the wave has in flight
+    // (vmcnt(0)).  A segment therefore takes all its rows at once, before it issues any store, and
+    // its phase-C stores go out after the next segment has taken its rows: the one wait per segment
+    // finds only long-issued operations in flight.  (A queue shifted by one row per step waited on
+    // every row for the previous row's stores.)
+    constexpr int RPS = SEG / RL;
     // NBM: branches held per row (1, or 4 = the most supported; CPNA > 0: CPNA)
-    int32_t nx[PD][NBM][E];
+    int32_t nx[RPS][NBM][E];
     // one row of every branch (CPNA > 0: packed 12-bit words, CPNA branches)
     auto load_row = [&](int64_t n0, int32_t (&dst)[NBM][E]) {
         if constexpr (CPNA > 0) {
@@ -485,29 +491,71 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
             }
         }
     };
+    auto load_seg = [&](int g) {
 #pragma unroll
-    for (int p = 0; p < PD; ++p) load_row((int64_t)RL * p + E * lane, nx[p]);
+        for (int j = 0; j < RPS; ++j)
+            if (g * RPS + j < nrows) load_row((int64_t)RL * (g * RPS + j) + E * lane, nx[j]);
+    };
+    load_seg(0);
+    // phase-C stores of a lane's chunk (issued one segment late, see above)
+    auto store_chunk = [&](int64_t c0, const double (&own)[SC], const bool (&abv)[SC]) {
+        if (vec_st && c0 + SC <= T) {
+            // whole chunk (T % SC == 0, flag buffer dword-aligned): 16-byte stores, one packed flag word
+            const int64_t gi = row_off + c0;
+#pragma unroll
+            for (int e = 0; e < SC; e += 2) {
+                if (a.smooth) *reinterpret_cast<double2*>(a.smooth + gi + e) = make_double2(own[e], own[e + 1]);
+                if (a.corr_scaled)
+                    *reinterpret_cast<double2*>(a.corr_scaled + gi + e) = make_double2(own[e] * scale, own[e + 1] * scale);
+            }
+            if (a.above) {
+                if constexpr (SC == 4) {
+                    *reinterpret_cast<uint32_t*>(a.above + gi) =
+                        (uint32_t)abv[0] | ((uint32_t)abv[1] << 8) | ((uint32_t)abv[2] << 16) | ((uint32_t)abv[3] << 24);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < SC; ++e) a.above[gi + e] = (uint8_t)abv[e];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < SC; ++e) {
+                const int64_t p = c0 + e;
+                if (p < T) {
+                    const int64_t gi = row_off + p;
+                    if (a.smooth) a.smooth[gi] = own[e];
+                    if (a.corr_scaled) a.corr_scaled[gi] = own[e] * scale;
+                    if (a.above) a.above[gi] = (uint8_t)abv[e];
+                }
+            }
+        }
+    };
+    bool pend = false;                                             // a chunk's stores deferred
+    int64_t pend_c0 = 0;
+    double pend_own[SC];
+    bool pend_abv[SC];
 
     const int nseg = (int)((T + SEG - 1) / SEG);
     for (int g = 0; g < nseg; ++g) {
         const int64_t s0 = (int64_t)SEG * g;
-        const int k0 = g * (SEG / RL), k1 = min(nrows, (g + 1) * (SEG / RL));
-        // ---------------- phase A: metric rows of the segment (stores of the metric arrays) ----
-        for (int k = k0; k < k1; ++k) {
-            const int nb = RL * k + E * lane;
-            const int xsl = k % MW;
-            int32_t cur[NBM][E];
+        const int k0 = g * RPS, k1 = min(nrows, (g + 1) * RPS);
+        int32_t rows[RPS][NBM][E];                                 // the segment's rows, taken at once
+#pragma unroll
+        for (int j = 0; j < RPS; ++j)
 #pragma unroll
             for (int t = 0; t < NBM; ++t)
 #pragma unroll
-                for (int e = 0; e < E; ++e) cur[t][e] = nx[0][t][e];
+                for (int e = 0; e < E; ++e) rows[j][t][e] = nx[j][t][e];
+        if (g + 1 < nseg) load_seg(g + 1);
+        if (pend) { store_chunk(pend_c0, pend_own, pend_abv); pend = false; }
+        // ---------------- phase A: metric rows of the segment (stores of the metric arrays) ----
 #pragma unroll
-            for (int p = 0; p + 1 < PD; ++p)
-#pragma unroll
-                for (int t = 0; t < NBM; ++t)
-#pragma unroll
-                    for (int e = 0; e < E; ++e) nx[p][t][e] = nx[p + 1][t][e];
-            if (k + PD < nrows) load_row((int64_t)RL * (k + PD) + E * lane, nx[PD - 1]);
+        for (int j = 0; j < RPS; ++j) {
+            const int k = k0 + j;
+            if (k >= k1) break;
+            const int nb = RL * k + E * lane;
+            const int xsl = k % MW;
+            const int32_t (&cur)[NBM][E] = rows[j];
             // Products and energies of 12-bit words are integers below 2^23 per sample and branch: for
             // <= 2 branches a row's prefix stays below 2^31 (2 x 2^23 x 64·E), so while every word seen
             // so far is 12-bit (sticky, wave-uniform check; int16 input may carry wider words) the row
@@ -763,37 +811,11 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 abv[e] = p >= vstart && p < T && (own[e] * scale >= hes[at]);      // minn_rtl.py:717-722
             }
         }
-        // ---------- phase C: gate and stores -----------------------------------------------------
-        if (vec_st && c0 + SC <= T) {
-            // whole chunk (T % SC == 0, flag buffer dword-aligned): 16-byte stores, one packed flag word
-            const int64_t gi = row_off + c0;
+        // ---------- phase C: gate; the chunk's stores wait for the next segment's row take -----------
+        pend = true;
+        pend_c0 = c0;
 #pragma unroll
-            for (int e = 0; e < SC; e += 2) {
-                if (a.smooth) *reinterpret_cast<double2*>(a.smooth + gi + e) = make_double2(own[e], own[e + 1]);
-                if (a.corr_scaled)
-                    *reinterpret_cast<double2*>(a.corr_scaled + gi + e) = make_double2(own[e] * scale, own[e + 1] * scale);
-            }
-            if (a.above) {
-                if constexpr (SC == 4) {
-                    *reinterpret_cast<uint32_t*>(a.above + gi) =
-                        (uint32_t)abv[0] | ((uint32_t)abv[1] << 8) | ((uint32_t)abv[2] << 16) | ((uint32_t)abv[3] << 24);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < SC; ++e) a.above[gi + e] = (uint8_t)abv[e];
-                }
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < SC; ++e) {
-                const int64_t p = c0 + e;
-                if (p < T) {
-                    const int64_t gi = row_off + p;
-                    if (a.smooth) a.smooth[gi] = own[e];
-                    if (a.corr_scaled) a.corr_scaled[gi] = own[e] * scale;
-                    if (a.above) a.above[gi] = (uint8_t)abv[e];
-                }
-            }
-        }
+        for (int e = 0; e < SC; ++e) { pend_own[e] = own[e]; pend_abv[e] = abv[e]; }
         if (a.detect && send > vstart) {
             double none[SC];
 #pragma unroll
@@ -802,6 +824,7 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
         }
         __builtin_amdgcn_wave_barrier();                               // LDS reuse by the next segment
     }
+    if (pend) store_chunk(pend_c0, pend_own, pend_abv);
     if (a.detect) gate.finish(lane, (int)T, a.n_ev + b, a.open_start ? a.open_start + b : nullptr);
 #if OFS_RTL_ROUNDS_DEBUG                    // tools/rtl_rounds.py: speculation rounds over the stream
     __builtin_amdgcn_wave_barrier();

@@ -93,6 +93,33 @@ __device__ __forceinline__ double row_sum(double v) {
     return v;
 }
 
+// DPP move into the lanes of the banks in BANK (4-lane groups of a 16-lane row), `old` elsewhere
+template <int CTRL, int BANK>
+__device__ __forceinline__ double dpp_d_bank(double old, double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, 0xf, BANK, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, 0xf, BANK, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Sums over the LPC lanes of a row of two steps' values at once (v0: step u, v1: step u + 1): the
+// first stage pairs the row's lower half with its upper half and each side keeps one step (lower:
+// u, upper: u + 1) and adds the partner's value of that step, so the remaining stages reduce ONE
+// value: 1 + log2(LPC/2) stages for both steps instead of 2·log2(LPC).  Result: the lower half of
+// the row holds Σ v0, the upper half Σ v1.
+template <int LPC>
+__device__ __forceinline__ double row_sum2(double v0, double v1) {
+    constexpr int SWAP = LPC == 16 ? 0x128 : 0x141;   // row_ror:8 | row_half_mirror (lane i <-> 7 - i)
+    constexpr int LO = LPC == 16 ? 0x3 : 0x5;         // banks of the lower half: 0,1 | 0,2
+    constexpr int HI = 0xf ^ LO;
+    const double keep = dpp_d_bank<0xE4, LO>(v1, v0);  // quad_perm identity: v0 in the lower half, else v1
+    const double recv = dpp_d_bank<SWAP, HI>(dpp_d_bank<SWAP, LO>(v0, v0), v1);
+    double v = keep + recv;
+    v += ofs::dpp_d<0xB1>(v);                         // quad_perm [1,0,3,2]
+    v += ofs::dpp_d<0x4E>(v);                         // quad_perm [2,3,0,1]
+    if constexpr (LPC == 16) v += ofs::dpp_d<0x141>(v);   // row_half_mirror within the 8-lane half
+    return v;
+}
+
 constexpr int ZS_G = 16;               // steps per group (one d staging, one store round)
 // per-wave staging entries per branch: one block (phase 1), two half blocks (the pair kernel's
 // phase 1) or ZS_G steps of d per row (phase 2)
@@ -592,36 +619,33 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
         }
         return;
     }
-    constexpr int KEEP = ZS_G / LPC;
+    // steps u, u + 1 reduced together (row_sum2): the lower half of the row ends with step u, the upper
+    // half with u + 1, so lane (hi, pos) keeps the steps 2(pos + HALF·j) + hi of the group
+    constexpr int HALF = LPC / 2, KEEP = ZS_G / LPC;
+    const int hi = sl / HALF, pos = sl % HALF;
     for (int og = 0; og < C; og += ZS_G) {
         zs_stage_d<FMT, NB, LPC, ROWS>(a, dbuf, b, o0, og, live, row, sl);
         wave_sync();
         double keep_n[KEEP], keep_e[KEEP];
 #pragma unroll
         for (int j = 0; j < KEEP; ++j) { keep_n[j] = 0.0; keep_e[j] = 0.0; }
-        auto reduce_keep = [&](double cr, double ci, double e, int u) {
-            cr = row_sum<LPC>(cr);
-            ci = row_sum<LPC>(ci);
-            e = row_sum<LPC>(e);
+#pragma unroll 1
+        for (int u = 0; u < ZS_G; u += 2) {
+            double cr0, ci0, e0, cr1, ci1, e1;
+            step_terms(g, h, cr0, ci0, e0);
+            advance(g, h, u);
+            step_terms(h, g, cr1, ci1, e1);
+            advance(h, g, u + 1);
+            const double cr = row_sum2<LPC>(cr0, cr1), ci = row_sum2<LPC>(ci0, ci1), e = row_sum2<LPC>(e0, e1);
             const double n2 = fma(cr, cr, ci * ci);
 #pragma unroll
             for (int j = 0; j < KEEP; ++j)
-                if (u == sl + LPC * j) { keep_n[j] = n2; keep_e[j] = e; }
-        };
-#pragma unroll 1
-        for (int u = 0; u < ZS_G; u += 2) {
-            double cr, ci, e;
-            step_terms(g, h, cr, ci, e);
-            reduce_keep(cr, ci, e, u);
-            advance(g, h, u);
-            step_terms(h, g, cr, ci, e);
-            reduce_keep(cr, ci, e, u + 1);
-            advance(h, g, u + 1);
+                if (u / 2 == pos + HALF * j) { keep_n[j] = n2; keep_e[j] = e; }
         }
         wave_sync();
 #pragma unroll
         for (int j = 0; j < KEEP; ++j) {
-            const int64_t s = o0 + og + sl + LPC * j;
+            const int64_t s = o0 + og + 2 * (pos + HALF * j) + hi;
             if (live && s < a.noff) {
                 const double den = a.t_energy * keep_e[j];
                 out[s] = (OUT)(keep_n[j] / (den > 1e-12 ? den : 1e-12));

@@ -15,6 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from ofdm_sync_amd import _lib, synth  # noqa: E402
@@ -31,9 +32,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--detect-only", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="variants may differ in rounding (no bit-equality check)")
-    ap.add_argument("--op", choices=("aa", "scminn", "sc", "comb", "minn"), default="aa", help="aa: ofs_aa_detect; scminn: "
-                    "ofs_sc_minn_metric (cfg4 fused S&C + Minn, N = 2 L)")
+    ap.add_argument("--op", choices=("aa", "scminn", "sc", "comb", "minn", "zcfreq"), default="aa",
+                    help="aa: ofs_aa_detect; scminn: ofs_sc_minn_metric (cfg4 fused S&C + Minn, N = 2 L); zcfreq: "
+                         "ofs_zc_freq_metric on c64 -> f32 (--na branches, N = 4 L, cp = L, the ZC template)")
     a = ap.parse_args()
+    if a.op == "zcfreq":
+        return zcfreq(a)
     if a.op != "aa":
         return scminn(a)
     dev = torch.device("cuda", 0)
@@ -132,6 +136,53 @@ def scminn(a):
         print(json.dumps(dict(lib=name, op=a.op, shape=[B, nb, T, N], ms_median=round(ms, 4),
                               ms_all=[round(t, 4) for t in times[name]], frac=round(alg / (ms / 1e3) / 8e12, 4))),
               flush=True)
+
+
+def zcfreq(a):
+    """zc_freq on the reference's stream shape by default (--B 4096 --na 2 --T 4242 --L 512: N 2048,
+    cp 512); outputs compared within 1e-12 relative (libraries may order the row sums differently)."""
+    from ofdm_sync_amd import zc_freq
+    dev = torch.device("cuda", 0)
+    B, nb, T, N, cp = a.B, a.na, a.T, 4 * a.L, a.L
+    g = torch.Generator(device=dev).manual_seed(8)
+    x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    idx, tb, e = zc_freq.make_pss_frequency_template()
+    idx = np.ascontiguousarray(np.asarray(idx, np.int32))
+    tb = np.ascontiguousarray(np.asarray(tb, np.complex128))
+    noff = T - (N + cp) + 1
+    out = torch.empty((B, noff), dtype=torch.float32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    libs = []
+    for p in a.libs.split(","):
+        l = ctypes.CDLL(os.path.abspath(p))
+        _lib._declare(l)
+        libs.append((os.path.basename(p), l))
+    call = lambda l: l.ofs_zc_freq_metric(_lib.C64, x.data_ptr(), B, nb, T, N, cp, _lib.FP32, int(idx.size),
+                                          idx.ctypes.data, tb.ctypes.data, float(e), out.data_ptr(), st.cuda_stream)
+    times = {n: [] for n, _ in libs}
+    ref = None
+    for r in range(a.rounds):
+        for name, l in libs[r % len(libs):] + libs[:r % len(libs)]:
+            out.fill_(float("nan"))
+            for _ in range(3):
+                assert call(l) == 0
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.steps):
+                call(l)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / a.steps)
+            if ref is None:
+                ref = out.double().clone()
+            elif not a.no_check:
+                d = ((out.double() - ref).abs() / ref.abs().clamp_min(1e-30)).max().item()
+                assert d <= 1e-6, f"{name}: metric differs by {d:.3g} relative"
+    for name, _ in libs:
+        ms = statistics.median(times[name])
+        print(json.dumps(dict(lib=name, op=a.op, shape=[B, nb, T, N, cp], ms_median=round(ms, 4),
+                              ms_all=[round(t, 4) for t in times[name]])), flush=True)
 
 
 if __name__ == "__main__":
