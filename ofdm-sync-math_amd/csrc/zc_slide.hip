@@ -541,26 +541,45 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
     // one offset: in-lane partials (numerator, energy) of the lane's pairs from (cur, prv) = (g, h)
     // or (h, g); the update writes the new g over prv, so two consecutive steps swap the roles of the
     // two register sets and no state is copied
+    // sg[q] (two branches): the branch sum of the set that is `prv` in the coming step - a step's h
+    // sums are the previous step's g sums, so each step forms only the g sums
+    double2 sg[NB > 1 ? PPL : 1];
+#pragma unroll
+    for (int q = 0; q < (NB > 1 ? PPL : 0); ++q) {
+        double sx = h[q][0].x, sy = h[q][0].y;
+#pragma unroll
+        for (int r = 1; r < NB; ++r) { sx += h[q][r].x; sy += h[q][r].y; }
+        sg[q] = make_double2(sx, sy);
+    }
+    // e: HALF the energy (|g|² + |h|² - c2·Re(g h*) summed); the factor 2 sits in the denominator
     auto step_terms = [&](const double2 (&cur)[PPL][NB], const double2 (&prv)[PPL][NB], double& cr, double& ci,
                           double& e) {
         double ep = 0.0, ed = 0.0;
         cr = 0.0; ci = 0.0;
 #pragma unroll
         for (int q = 0; q < PPL; ++q) {
-            double gr = cur[q][0].x, gim = cur[q][0].y, hr = prv[q][0].x, him = prv[q][0].y;
+            double gr = cur[q][0].x, gim = cur[q][0].y;
 #pragma unroll
-            for (int r = 1; r < NB; ++r) { gr += cur[q][r].x; gim += cur[q][r].y; hr += prv[q][r].x; him += prv[q][r].y; }
+            for (int r = 1; r < NB; ++r) { gr += cur[q][r].x; gim += cur[q][r].y; }
+            double hr = prv[q][0].x, him = prv[q][0].y;
+            if constexpr (NB > 1) {
+                hr = sg[q].x; him = sg[q].y;
+                sg[q] = make_double2(gr, gim);
+            }
             cr = fma(A[q].x, gr, fma(-A[q].y, gim, fma(Bc[q].x, hr, fma(-Bc[q].y, him, cr))));
             ci = fma(A[q].x, gim, fma(A[q].y, gr, fma(Bc[q].x, him, fma(Bc[q].y, hr, ci))));
+            double t = cur[q][0].y * prv[q][0].y;                      // Σ_br Re(g h*)
+            t = fma(cur[q][0].x, prv[q][0].x, t);
 #pragma unroll
-            for (int r = 0; r < NB; ++r) {
-                ep = fma(cur[q][r].x, cur[q][r].x, fma(cur[q][r].y, cur[q][r].y, ep));
-                ed = fma(c2[q], fma(cur[q][r].x, prv[q][r].x, cur[q][r].y * prv[q][r].y), ed);
-            }
+            for (int r = 1; r < NB; ++r) t = fma(cur[q][r].x, prv[q][r].x, fma(cur[q][r].y, prv[q][r].y, t));
+#pragma unroll
+            for (int r = 0; r < NB; ++r) ep = fma(cur[q][r].x, cur[q][r].x, fma(cur[q][r].y, cur[q][r].y, ep));
+            ed = fma(c2[q], t, ed);
         }
-        e = 2.0 * (ep + epp - ed);
+        e = (ep + epp) - ed;
         epp = ep;
     };
+    const double te2 = 2.0 * a.t_energy;                               // template energy x the energy's 2
     auto advance = [&](const double2 (&cur)[PPL][NB], double2 (&prv)[PPL][NB], int u) {
 #pragma unroll
         for (int r = 0; r < NB; ++r) {
@@ -610,7 +629,7 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
                     }
                     const int64_t s = o0 + og + v * ZS_RG + sl;
                     if (live && s < a.noff) {
-                        const double den = a.t_energy * se;
+                        const double den = te2 * se;
                         out[s] = (OUT)(fma(sr, sr, si * si) / (den > 1e-12 ? den : 1e-12));
                     }
                 }
@@ -647,7 +666,7 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
         for (int j = 0; j < KEEP; ++j) {
             const int64_t s = o0 + og + 2 * (pos + HALF * j) + hi;
             if (live && s < a.noff) {
-                const double den = a.t_energy * keep_e[j];
+                const double den = te2 * keep_e[j];
                 out[s] = (OUT)(keep_n[j] / (den > 1e-12 ? den : 1e-12));
             }
         }
