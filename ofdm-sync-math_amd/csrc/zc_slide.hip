@@ -120,6 +120,21 @@ __device__ __forceinline__ double row_sum2(double v0, double v1) {
     return v;
 }
 
+// Sums over a 16-lane row of four steps' values (v0..v3: steps u..u+3) by two reduce-scatter stages:
+// row_ror:8 (lanes 0-7 keep steps u, u+1, lanes 8-15 steps u+2, u+3), then row_half_mirror (lane i
+// <-> 7 - i: banks 0/2 keep the first of their two steps, banks 1/3 the second), then two quad
+// stages on ONE value: 6 stages for four steps instead of 16.  Bank q of the row (lanes 4q..4q+3)
+// ends with Σ v_q.
+__device__ __forceinline__ double row_sum4(double v0, double v1, double v2, double v3) {
+    const double k0 = dpp_d_bank<0xE4, 0x3>(v2, v0), k1 = dpp_d_bank<0xE4, 0x3>(v3, v1);
+    const double a0 = k0 + dpp_d_bank<0x128, 0xC>(dpp_d_bank<0x128, 0x3>(v0, v0), v2);
+    const double a1 = k1 + dpp_d_bank<0x128, 0xC>(dpp_d_bank<0x128, 0x3>(v1, v1), v3);
+    double v = dpp_d_bank<0xE4, 0x5>(a1, a0) + dpp_d_bank<0x141, 0xA>(dpp_d_bank<0x141, 0x5>(a0, a0), a1);
+    v += ofs::dpp_d<0xB1>(v);                         // quad_perm [1,0,3,2]
+    v += ofs::dpp_d<0x4E>(v);                         // quad_perm [2,3,0,1]
+    return v;
+}
+
 constexpr int ZS_G = 16;               // steps per group (one d staging, one store round)
 // per-wave staging entries per branch: one block (phase 1), two half blocks (the pair kernel's
 // phase 1) or ZS_G steps of d per row (phase 2)
@@ -640,8 +655,10 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
     }
     // steps u, u + 1 reduced together (row_sum2): the lower half of the row ends with step u, the upper
     // half with u + 1, so lane (hi, pos) keeps the steps 2(pos + HALF·j) + hi of the group
-    constexpr int HALF = LPC / 2, KEEP = ZS_G / LPC;
-    const int hi = sl / HALF, pos = sl % HALF;
+    // STEPS consecutive steps reduced together (row_sum2 / row_sum4): lane (which, pos) of the row ends
+    // with step u + which and keeps the steps STEPS·(pos + SPAN·j) + which of the group
+    constexpr int STEPS = LPC == 16 ? 4 : 2, SPAN = LPC / STEPS, KEEP = ZS_G / LPC;
+    const int which = sl / SPAN, pos = sl % SPAN;
     for (int og = 0; og < C; og += ZS_G) {
         zs_stage_d<FMT, NB, LPC, ROWS>(a, dbuf, b, o0, og, live, row, sl);
         wave_sync();
@@ -649,22 +666,40 @@ __global__ __launch_bounds__(64 * ZS_MAXW) void zc_pair_kernel(ZsArgs a) {
 #pragma unroll
         for (int j = 0; j < KEEP; ++j) { keep_n[j] = 0.0; keep_e[j] = 0.0; }
 #pragma unroll 1
-        for (int u = 0; u < ZS_G; u += 2) {
-            double cr0, ci0, e0, cr1, ci1, e1;
-            step_terms(g, h, cr0, ci0, e0);
-            advance(g, h, u);
-            step_terms(h, g, cr1, ci1, e1);
-            advance(h, g, u + 1);
-            const double cr = row_sum2<LPC>(cr0, cr1), ci = row_sum2<LPC>(ci0, ci1), e = row_sum2<LPC>(e0, e1);
+        for (int u = 0; u < ZS_G; u += STEPS) {
+            double cr, ci, e;
+            if constexpr (STEPS == 4) {
+                double cr0, ci0, e0, cr1, ci1, e1, cr2, ci2, e2, cr3, ci3, e3;
+                step_terms(g, h, cr0, ci0, e0);
+                advance(g, h, u);
+                step_terms(h, g, cr1, ci1, e1);
+                advance(h, g, u + 1);
+                step_terms(g, h, cr2, ci2, e2);
+                advance(g, h, u + 2);
+                step_terms(h, g, cr3, ci3, e3);
+                advance(h, g, u + 3);
+                cr = row_sum4(cr0, cr1, cr2, cr3);
+                ci = row_sum4(ci0, ci1, ci2, ci3);
+                e = row_sum4(e0, e1, e2, e3);
+            } else {
+                double cr0, ci0, e0, cr1, ci1, e1;
+                step_terms(g, h, cr0, ci0, e0);
+                advance(g, h, u);
+                step_terms(h, g, cr1, ci1, e1);
+                advance(h, g, u + 1);
+                cr = row_sum2<LPC>(cr0, cr1);
+                ci = row_sum2<LPC>(ci0, ci1);
+                e = row_sum2<LPC>(e0, e1);
+            }
             const double n2 = fma(cr, cr, ci * ci);
 #pragma unroll
             for (int j = 0; j < KEEP; ++j)
-                if (u / 2 == pos + HALF * j) { keep_n[j] = n2; keep_e[j] = e; }
+                if (u / STEPS == pos + SPAN * j) { keep_n[j] = n2; keep_e[j] = e; }
         }
         wave_sync();
 #pragma unroll
         for (int j = 0; j < KEEP; ++j) {
-            const int64_t s = o0 + og + 2 * (pos + HALF * j) + hi;
+            const int64_t s = o0 + og + STEPS * (pos + SPAN * j) + which;
             if (live && s < a.noff) {
                 const double den = te2 * keep_e[j];
                 out[s] = (OUT)(keep_n[j] / (den > 1e-12 ? den : 1e-12));
