@@ -776,7 +776,10 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                 // reference recursion over its chunk from `enter`, then takes lane-1's leaving
                 // state (DPP wave_shr:1) as its new `enter`; stop when no lane's entering state
                 // changes.  Lane 0 starts exact, and after round r lanes 0..r are exact: <= 64 rounds.
-                for (int round = 0; round <= 64; ++round) {
+#ifndef OFS_RTL_MAXROUNDS                   // diagnostic builds only: < 64 cuts the rounds (inexact)
+#define OFS_RTL_MAXROUNDS 64
+#endif
+                for (int round = 0; round <= OFS_RTL_MAXROUNDS; ++round) {
                     double st = enter;
                     if (fast) {
 #pragma unroll
