@@ -38,9 +38,20 @@ _DIST = None                     # torch.distributed when run with N ranks (barr
 _LAST_HOST_MS = None             # host time per step of the last timed() (enqueue only; > ms = host-bound)
 
 
+WARM_MS = 100.0      # untimed calls continue until this much wall time has passed (clock ramp)
+
+
 def timed(step, steps, warmup, stream):
-    for _ in range(warmup):
+    """HIP events over `steps` calls after `warmup` untimed calls, continued until WARM_MS of wall
+    time have passed: sub-millisecond kernels reach steady clocks only after some tens of ms of load
+    (zc_freq_refshape 0.62 ms after 5 calls vs 0.553 ms steady, tools/lib_ab.py rounds)."""
+    t_w = time.perf_counter()
+    n = 0
+    while n < warmup or (time.perf_counter() - t_w) * 1e3 < WARM_MS:
         step()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if _DIST is not None:
         _DIST.barrier()
@@ -645,9 +656,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default=",".join(CONFIGS))
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5, help="untimed calls first (sub-ms kernels need a few "
-                                                          "to reach steady clocks: zc_freq_refshape 0.76 "
-                                                          "ms on the first timed pass vs 0.63 steady)")
+    ap.add_argument("--warmup", type=int, default=5, help="untimed calls first, at least; they continue until "
+                                                          "WARM_MS of wall time (sub-ms kernels reach steady "
+                                                          "clocks only after tens of ms of load)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--cfg4-global", type=int, default=262144, help="cfg4 streams over all GPUs")
     ap.add_argument("--cfg5-global", type=int, default=1 << 20, help="cfg5 sequences over all GPUs")
