@@ -779,30 +779,56 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #ifndef OFS_RTL_MAXROUNDS                   // diagnostic builds only: < 64 cuts the rounds (inexact)
 #define OFS_RTL_MAXROUNDS 64
 #endif
-                for (int round = 0; round <= OFS_RTL_MAXROUNDS; ++round) {
-                    double st = enter;
-                    if (fast) {
+                // Fast segments test the chain every second round: the untested round's hand-over and
+                // the tested round's are the same operation, and a consistent tested round is the
+                // reference trajectory as before; the test (compare, ballot, scalar branch) is what the
+                // pair saves, at most one extra round per segment.
+#ifndef OFS_RTL_RPT
+#define OFS_RTL_RPT 2                      // rounds per consistency test on fast segments (tuning builds)
+#endif
+                if (fast) {
+                    for (int round = 0; round <= OFS_RTL_MAXROUNDS; round += OFS_RTL_RPT) {
+                        double st = enter;
+#pragma unroll
+                        for (int r = 1; r < OFS_RTL_RPT; ++r) {            // untested rounds
+#pragma unroll
+                            for (int e = 0; e < SC; ++e) st = fma(cv[e] - st, inv, st);
+                            enter = ofs::wave_shr1(st, lane, sm);
+                            st = enter;
+                        }
 #pragma unroll
                         for (int e = 0; e < SC; ++e) {
                             st = fma(cv[e] - st, inv, st);
                             own[e] = st;
                         }
-                    } else {
+                        const double prev_leave = ofs::wave_shr1(st, lane, sm);
+#if OFS_RTL_ROUNDS_DEBUG
+                        dbg_rounds += OFS_RTL_RPT;
+#endif
+                        if (__ballot(!same_bits(enter, prev_leave)) == 0) {
+                            sm = readlane(st, 63);
+                            break;
+                        }
+                        enter = prev_leave;
+                    }
+                } else {
+                    for (int round = 0; round <= OFS_RTL_MAXROUNDS; ++round) {
+                        double st = enter;
 #pragma unroll
                         for (int e = 0; e < SC; ++e) {
                             if (upd[e]) st = st + (cv[e] - st) * inv;
                             own[e] = st;
                         }
-                    }
-                    const double prev_leave = ofs::wave_shr1(st, lane, sm);
+                        const double prev_leave = ofs::wave_shr1(st, lane, sm);
 #if OFS_RTL_ROUNDS_DEBUG
-                    ++dbg_rounds;
+                        ++dbg_rounds;
 #endif
-                    if (__ballot(!same_bits(enter, prev_leave)) == 0) {
-                        sm = readlane(st, 63);
-                        break;
+                        if (__ballot(!same_bits(enter, prev_leave)) == 0) {
+                            sm = readlane(st, 63);
+                            break;
+                        }
+                        enter = prev_leave;
                     }
-                    enter = prev_leave;
                 }
             }
             // ---------- phase C: threshold (chunk layout) -----------------------------------------
