@@ -779,12 +779,13 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
 #ifndef OFS_RTL_MAXROUNDS                   // diagnostic builds only: < 64 cuts the rounds (inexact)
 #define OFS_RTL_MAXROUNDS 64
 #endif
-                // Fast segments test the chain every second round: the untested round's hand-over and
-                // the tested round's are the same operation, and a consistent tested round is the
+                // Fast segments test the chain every OFS_RTL_RPT-th round: an untested round's hand-over
+                // and the tested round's are the same operation, and a consistent tested round is the
                 // reference trajectory as before; the test (compare, ballot, scalar branch) is what the
-                // pair saves, at most one extra round per segment.
+                // group saves, at most RPT - 1 extra rounds per segment (RPT 1 / 2 / 3 / 4: cfg2b 0.048
+                // / 0.043 / 0.0414 / 0.0413 ms, profiles/r04t_*).
 #ifndef OFS_RTL_RPT
-#define OFS_RTL_RPT 2                      // rounds per consistency test on fast segments (tuning builds)
+#define OFS_RTL_RPT 4                      // rounds per consistency test on fast segments (tuning builds)
 #endif
                 if (fast) {
                     for (int round = 0; round <= OFS_RTL_MAXROUNDS; round += OFS_RTL_RPT) {
