@@ -96,8 +96,9 @@ const char* ofs_status_string(int32_t status);
  *   ZC_NODMA     1: zc_v2 CFAR tiles through registers instead of LDS-DMA
  *   BE_FAST      0: receiver back-end through the generic kernel
  * ofs_debug_set_variant returns OFS_EINVAL for an unknown name; value OFS_VARIANT_UNSET clears
- * one variant, ofs_debug_reset_variants clears all.  Not for concurrent use with running calls
- * (a call reads each variant once, at dispatch).
+ * one variant, ofs_debug_reset_variants clears all.  The table is per calling thread
+ * (thread_local): a variant set by one thread steers only the calls that same thread makes, and
+ * every new thread starts with all variants unset.  A call reads each variant once, at dispatch.
  */
 #define OFS_VARIANT_UNSET INT64_MIN
 int32_t ofs_debug_set_variant(const char* name, int64_t value);

@@ -1205,7 +1205,9 @@ int32_t ofs_zc_freq_metric(int32_t in_fmt, const void* x, int64_t B, int32_t n_b
 int32_t ofs_zc_freq_partial(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64_t T, int32_t br0,
                             int32_t n_grp, int32_t N, int32_t cp, int32_t n_bins, const int32_t* bin_indices,
                             const double* template_bins, int32_t accumulate, double* part, void* stream) {
-    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * T) || OFS_MISSING(part, B) || !bin_indices || !template_bins || B < 0 ||
+    const int64_t noff_ = T - ((int64_t)N + cp) + 1;            // x: [B][n_br][T], part: [B][noff][3]
+    if (!fmt_ok(in_fmt) || OFS_MISSING(x, B * n_br * T) || OFS_MISSING(part, B * (noff_ > 0 ? noff_ : 1)) ||
+        !bin_indices || !template_bins || B < 0 ||
         n_br < 1 || br0 < 0 || n_grp < 1 || n_grp > 4 || br0 + n_grp > n_br || T < 0 || N < 1 || cp < 0 ||
         n_bins < 1 || n_bins > 64)
         return OFS_EINVAL;

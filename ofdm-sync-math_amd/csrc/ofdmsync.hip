@@ -817,8 +817,13 @@ static const char* const kVariantNames[ofs::V_COUNT] = {
     "EXACT", "FAST_E", "FAST_E_DO", "FAST_SCAN", "FAST_SCAN_DO", "RTL_WPB", "PARK_DIRECT", "ZW64",
     "ZW64_GRID", "ZS", "ZF_ITEMS", "ZS_PAIR", "ZS_DEFER", "ZS_BPL", "ZS_C", "ZS_GBLK", "MC_FUSED",
     "MC_FUSE_X", "ZC_SEQ", "ZC_NODMA", "BE_FAST"};
-static std::atomic<int64_t> g_variants[ofs::V_COUNT] = {};
-static std::atomic<bool> g_variants_init{false};
+// Per calling thread: a variant one thread sets steers only the calls that thread makes, so
+// concurrent callers (another thread's production calls) never see a test's forced kernel.
+struct VariantTable {
+    int64_t v[ofs::V_COUNT];
+    VariantTable() { for (auto& x : v) x = OFS_VARIANT_UNSET; }
+};
+static thread_local VariantTable g_variants;
 
 static int variant_index(const char* name) {
     if (!name) return -1;
@@ -828,16 +833,14 @@ static int variant_index(const char* name) {
 }
 
 int32_t ofs_debug_reset_variants(void) {
-    for (auto& v : g_variants) v.store(OFS_VARIANT_UNSET, std::memory_order_relaxed);
-    g_variants_init.store(true, std::memory_order_release);
+    for (auto& x : g_variants.v) x = OFS_VARIANT_UNSET;
     return OFS_OK;
 }
 
 int32_t ofs_debug_set_variant(const char* name, int64_t value) {
     const int i = variant_index(name);
     if (i < 0) return OFS_EINVAL;
-    if (!g_variants_init.load(std::memory_order_acquire)) ofs_debug_reset_variants();
-    g_variants[i].store(value, std::memory_order_relaxed);
+    g_variants.v[i] = value;
     return OFS_OK;
 }
 
@@ -1090,7 +1093,6 @@ int32_t ofs_cp_cfo(int32_t in_fmt, const void* x, int64_t B, int32_t n_br, int64
 
 namespace ofs {
 int64_t variant(Variant v) {
-    if (!g_variants_init.load(std::memory_order_acquire)) return OFS_VARIANT_UNSET;
-    return g_variants[v].load(std::memory_order_relaxed);
+    return g_variants.v[v];
 }
 }  // namespace ofs

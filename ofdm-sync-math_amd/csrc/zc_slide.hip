@@ -736,7 +736,12 @@ int zs_launch(K kern, bool& attr, const ZsArgs& a, size_t lds, hipStream_t st) {
 
 template <int FMT, int NB, class OUT>
 int zs_go(const ZsArgs& a, size_t lds, int bpl, bool pair, hipStream_t st) {
-    const bool df = zs_defer(NB);
+    bool df = zs_defer(NB);
+    // the pair kernel parks the waves' partials in its block region (one branch's blocks): where
+    // they would reach past it into the waves' staging, the per-step DPP row sums serve instead
+    if (pair && df && (size_t)a.W * ZS_RG * ZS_PS * sizeof(double) >
+                          (size_t)(bpl * a.W + a.N / a.C - 1) * 64 * sizeof(double2))
+        df = false;
     static bool at[6] = {false, false, false, false, false, false};
     if (pair) {
         constexpr int PPL = NB == 2 ? 2 : 4;          // rows of 32/PPL lanes: 4 chunks (two branches) / 8 per wave

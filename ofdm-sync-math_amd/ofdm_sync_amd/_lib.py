@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("OFS_LIB") or os.path.join(_HERE, "libofdmsync.so")   # OFS_LIB: tuning builds
+LIB_PATH = os.path.join(_HERE, "libofdmsync.so")       # the in-tree build (no environment override)
+TUNING_BUILD = None          # set by use_tuning_library(): name of the tools/variants.py build in use
 
 # input formats / precisions / status (include/ofdmsync.h)
 C64, C128, CI16, CP12 = 0, 1, 2, 3
@@ -140,8 +141,19 @@ def _declare(lib):
         fn.argtypes = args
 
 
+def _baked_hash(l) -> str:
+    fn = getattr(l, "ofs_source_hash", None)                # absent in libraries older than the check
+    if fn is None:
+        return "<none>"
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    return fn().decode()
+
+
 def lib():
-    """Load libofdmsync.so (after torch, so both share torch's HIP runtime)."""
+    """Load libofdmsync.so (after torch, so both share torch's HIP runtime).  The library must carry
+    the hash of the sources next to it (source_hash()); the one other library accepted is a tuning
+    build named explicitly through use_tuning_library()."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -149,18 +161,31 @@ def lib():
                 f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
                 "from the repository root (hipcc --offload-arch=gfx950)")
         l = ctypes.CDLL(LIB_PATH)
-        if not os.environ.get("OFS_LIB") and source_files():
-            fn = getattr(l, "ofs_source_hash", None)        # absent in libraries older than the check
-            if fn is not None:
-                fn.restype = ctypes.c_char_p
-                fn.argtypes = []
-            built, want = ("<none>" if fn is None else fn().decode()), source_hash()
+        if source_files():
+            built, want = _baked_hash(l), source_hash()
             if built != want:
                 raise ImportError(f"{LIB_PATH} was built from other sources (hash {built}, sources {want}); "
                                   "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
         _declare(l)
         _lib = l
     return _lib
+
+
+def use_tuning_library(path: str) -> str:
+    """Measurement tools only: load a tuning build of tools/variants.py (the sources compiled with
+    extra -D flags; its baked hash reads ``variant-<name>``) instead of the in-tree library.  Must
+    run before the library is first used; any other library is refused.  Returns the build name."""
+    global _lib, TUNING_BUILD
+    if _lib is not None:
+        raise RuntimeError("use_tuning_library() must run before the library is first loaded")
+    path = os.path.abspath(path)
+    l = ctypes.CDLL(path)
+    built = _baked_hash(l)
+    if not built.startswith("variant-"):
+        raise ImportError(f"{path} is not a tools/variants.py tuning build (hash {built})")
+    _declare(l)
+    _lib, TUNING_BUILD = l, built[len("variant-"):]
+    return TUNING_BUILD
 
 
 # ------------------------------------------------------------------------------------------

@@ -115,6 +115,32 @@ def _ref_dev(reference, r_host: np.ndarray, dev):
     return torch.from_numpy(r_host).to(dev), energy
 
 
+class MatchedFilter:
+    """A prepared reference for the batched correlation / detection entry points
+    (``correlate_batched``, ``detect_zc_preamble_batched``): its complex128 taps (host copy and a
+    device copy), its energy (zc_v2.py:263) and its content key for the FFT plan cache are computed
+    ONCE here.  A raw device tensor passed as ``reference`` is copied to the host and hashed on
+    every call (a stream synchronisation per call); a MatchedFilter skips that.  The taps are a
+    snapshot: later writes to the tensor it was built from do not reach it."""
+
+    def __init__(self, reference, device=None):
+        self.host = _ref_host(reference)
+        self.key = _ref_key(self.host)
+        self.energy = float(np.sum(np.abs(self.host) ** 2))
+        self.device = torch.device(device) if device is not None else _lib.require_gpu()
+        self.taps = torch.from_numpy(self.host).to(self.device)
+
+    def __len__(self) -> int:
+        return int(self.host.size)
+
+    def taps_on(self, dev) -> torch.Tensor:
+        return self.taps if self.taps.device == torch.device(dev) else self.taps.to(dev)
+
+    def correlate(self, x, mode: int = None, **kw):
+        """correlate_batched(x, self, mode, ...): mode defaults to OFS_ZC_V2 (|corr| normalised)."""
+        return correlate_batched(x, self, OFS_ZC_V2 if mode is None else mode, **kw)
+
+
 class MFPlan:
     """FFT overlap-save matched-filter plan (ofs_zc_mf_plan_create) for one reference and one
     batch shape [B, n_branch, T]: the rocFFT plans, the reference spectrum and the plan's rocFFT
@@ -184,11 +210,13 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     (overlap-save through rocFFT, fp64; raises if the shape has no plan); "auto": the FFT path
     for references of >= FFT_MIN_TAPS taps (measured 2048 taps: DESIGN.md §4.5b) in every mode
     but OFS_ZC_NORMALIZE, falling back to the direct sums for shapes the overlap-save extract
-    cannot hold (ofs_zc_mf_plan_create -> OFS_ETOOLONG: e.g. 4 branches at N = 2048)."""
+    cannot hold (ofs_zc_mf_plan_create -> OFS_ETOOLONG: e.g. 4 branches at N = 2048).
+    ``reference``: taps (numpy / tensor) or a MatchedFilter (no per-call host copy or hashing)."""
     batch = _lib.as_batch(x, batched=True)
     dev = batch.data.device
-    r_host = _ref_host(reference)
-    energy = float(np.sum(np.abs(r_host) ** 2))         # as the reference computes it (zc_v2.py:263)
+    mf = reference if isinstance(reference, MatchedFilter) else None
+    r_host = mf.host if mf is not None else _ref_host(reference)
+    energy = mf.energy if mf is not None else float(np.sum(np.abs(r_host) ** 2))   # zc_v2.py:263
     N = int(r_host.size)
     nout = batch.T + N - 1
     shape = (batch.B, batch.nb, nout) if mode == OFS_ZC_RAW else (batch.B, nout)
@@ -199,14 +227,15 @@ def correlate_batched(x, reference, mode: int, corr_in=None, want_corr=True, wan
     use_fft = mode != OFS_ZC_NORMALIZE and batch.B > 0 and batch.T > 0 and (
         method == "fft" or (method == "auto" and N >= FFT_MIN_TAPS))
     if use_fft:
-        plan = _mf_plan(r_host, _ref_key(r_host), batch.B, batch.nb, batch.T, dev)
+        plan = _mf_plan(r_host, mf.key if mf is not None else _ref_key(r_host), batch.B, batch.nb, batch.T, dev)
         if plan is not None:
             plan.run(batch, energy, mode, corr, mag)
             return corr, mag
         if method == "fft":
             raise RuntimeError(f"ofs_zc_mf_plan_create: no overlap-save plan for {batch.nb} branches x "
                                f"{N} taps (extract LDS); use method='direct' (status -2)")
-    ref, _ = _ref_dev(reference, r_host, dev)          # the direct sums read the taps on the device
+    # the direct sums read the taps on the device
+    ref = mf.taps_on(dev) if mf is not None else _ref_dev(reference, r_host, dev)[0]
     ci = None
     if mode == OFS_ZC_NORMALIZE:
         ci = torch.as_tensor(corr_in).to(device=dev, dtype=torch.complex128).reshape(batch.B, nout).contiguous()
@@ -334,7 +363,8 @@ def detect_zc_preamble_batched(x, reference=None, window_size: int = CORR_WINDOW
                                min_corr_mag: float = MIN_CORR_MAG, hysteresis: int = HYSTERESIS,
                                normalize: bool = True, max_events: int = 8,
                                want_state: bool = True) -> ZCBatchResult:
-    """detect_zc_preamble over x[B, n_branch, T]; everything stays on the device."""
+    """detect_zc_preamble over x[B, n_branch, T]; everything stays on the device.  ``reference``:
+    taps or a MatchedFilter (default: the PSS symbol of build_pss_symbol)."""
     if reference is None:
         reference = build_pss_symbol(include_cp=False)
     ref_len = int(len(reference))

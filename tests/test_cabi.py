@@ -156,3 +156,68 @@ def test_debug_variants_entry_point(lib):
     assert lib.ofs_debug_set_variant(b"EXACT", unset) == 0 and lib.ofs_debug_get_variant(b"EXACT") == unset
     assert lib.ofs_debug_reset_variants() == 0
     assert all(lib.ofs_debug_get_variant(n.encode()) == unset for n in names)
+
+
+def test_debug_variants_are_per_thread(lib):
+    """The variant table is thread_local: a variant forced by one thread (a test) is not seen by
+    calls another thread makes, and a new thread starts with every variant unset."""
+    import threading
+    from ofdm_sync_amd import _lib as L
+    L._declare(lib)
+    unset = -(1 << 63)
+    assert lib.ofs_debug_set_variant(b"EXACT", 0) == 0
+    seen = {}
+
+    def other():
+        seen["before"] = lib.ofs_debug_get_variant(b"EXACT")
+        lib.ofs_debug_set_variant(b"ZS_PAIR", 5)
+        seen["own"] = lib.ofs_debug_get_variant(b"ZS_PAIR")
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen == {"before": unset, "own": 5}
+    assert lib.ofs_debug_get_variant(b"EXACT") == 0
+    assert lib.ofs_debug_get_variant(b"ZS_PAIR") == unset
+    assert lib.ofs_debug_reset_variants() == 0
+
+
+def test_product_mirror_reads_no_environment():
+    """The Python mirror takes no switch from the environment: OFS_LIB (or any other variable)
+    cannot swap the library or skip its source-hash check."""
+    pkg = os.path.join(ROOT, "ofdm-sync-math_amd", "ofdm_sync_amd")
+    for f in sorted(os.listdir(pkg)):
+        if f.endswith(".py"):
+            txt = open(os.path.join(pkg, f)).read()
+            # shard.py reads the torch.distributed launch contract (RANK / WORLD_SIZE / LOCAL_RANK) only
+            names = set(re.findall(r"os\.environ\.get\(\"(\w+)\"", txt))
+            assert names <= ({"RANK", "WORLD_SIZE", "LOCAL_RANK"} if f == "shard.py" else set()), (f, names)
+            assert not re.search(r"os\.environ\[|getenv\s*\(", txt), f
+            assert len(re.findall(r"os\.environ", txt)) == len(re.findall(r"os\.environ\.get\(\"", txt)), f
+
+
+def test_library_path_ignores_ofs_lib_and_tuning_loader_refuses_product_build(tmp_path):
+    """In a fresh process with OFS_LIB pointing elsewhere, the mirror still loads the in-tree
+    library (hash-checked); use_tuning_library accepts only a tools/variants.py build (baked hash
+    variant-<name>), so it refuses the product library itself."""
+    import subprocess
+    import sys
+    if not os.path.exists(LIB):
+        import __graft_entry__ as g
+        g.build_hip()
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from ofdm_sync_amd import _lib\n"
+        "l = _lib.lib(); import os\n"
+        "assert os.path.samefile(l._name, %r), l._name\n"
+        "_lib._lib = None\n"
+        "try:\n"
+        "    _lib.use_tuning_library(%r)\n"
+        "except ImportError as e:\n"
+        "    print('refused', e)\n"
+        "else:\n"
+        "    raise SystemExit('accepted')\n"
+    ) % (os.path.join(ROOT, "ofdm-sync-math_amd"), LIB, LIB)
+    env = dict(os.environ, OFS_LIB=str(tmp_path / "nonexistent.so"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "refused" in r.stdout

@@ -360,7 +360,7 @@ def test_zc_freq_fp32_many_offsets_and_unsupported_shape():
                                            ("c64", 256, 64, 3001, 1), ("i16", 512, 0, 2600, 2),
                                            ("c128", 64, 16, 700, 1), ("c128", 4096, 1024, 9000, 1),
                                            ("c128", 8192, 0, 8300, 1), ("c128", 192, 5, 1000, 2),
-                                           ("c128", 2048, 512, 2600, 1)])
+                                           ("c128", 2048, 512, 2600, 1), ("c128", 2048, 512, 8000, 2)])
 def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, variant):
     """The block-initialised sliding DFT (zc_slide.hip, plan 4: the pair resonators for the ZC template's
     ±k bins) against the C oracle's fp64 FFTs on every window (1e-9 relative + 1e-11), against the
@@ -390,8 +390,11 @@ def test_zc_slide_kernel_vs_oracle_and_previous(fmt, N, cp, T, nb, variant):
     np.testing.assert_allclose(m, m_prev, rtol=1e-9, atol=1e-11)
     variant("ZS_DEFER", 0)        # per-step DPP row sums instead of the LDS partials
     m_dpp = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
+    variant("ZS_DEFER", 1)        # LDS partials forced (two branches: only where they fit the block region)
+    m_lds = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
     variant("ZS_DEFER", None)
     np.testing.assert_allclose(m, m_dpp, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(m, m_lds, rtol=1e-12, atol=1e-14)
     variant("ZS_PAIR", 0)         # first-order recursion per bin instead of the pair resonators
     m_bin = zc_freq.compute_frequency_metric_batched(xd, idx, t, e, N=N, cp=cp, precision="fp64").cpu().numpy()
     variant("ZS_PAIR", None)
@@ -515,6 +518,33 @@ def test_zc_fft_plan_cache_device_references_at_recycled_address():
             want = np.abs(O.normalize_correlation(O.matched_filter(x_r[b, 0], ref_h), x_r[b, 0], ref_h))
             np.testing.assert_allclose(mag[b], want, rtol=1e-9, atol=1e-12)
     assert len(set(ptrs)) < len(ptrs), "the allocator did not recycle the address; the test is vacuous"
+
+
+@pytest.mark.parametrize("method", ["fft", "direct"])
+def test_zc_matched_filter_handle_skips_host_copy(method, monkeypatch):
+    """zc_v2.MatchedFilter: the prepared reference gives the same correlation and detection as the
+    raw taps (bit for bit), and a call with it never copies / hashes the taps again (the per-call
+    device-to-host sync of a raw device reference): _ref_host is made to fail after construction."""
+    rng = np.random.default_rng(47)
+    ref_h = O.pss_symbol(2048, root=29)
+    x = rng_c(rng, 3, 1, 9000)
+    x[1, 0, 4000:4000 + ref_h.size] += 2 * ref_h
+    xd = torch.from_numpy(x).cuda()
+    mf = zc_v2.MatchedFilter(torch.as_tensor(ref_h, device="cuda"))
+    assert len(mf) == ref_h.size
+    want_c, want_m = zc_v2.correlate_batched(xd, ref_h, zc_v2.OFS_ZC_V2, want_mag=True, method=method)
+    want_d = zc_v2.detect_zc_preamble_batched(xd, ref_h)
+
+    def _no_copy(*a, **k):
+        raise AssertionError("reference copied to the host")
+    monkeypatch.setattr(zc_v2, "_ref_host", _no_copy)
+    got_c, got_m = zc_v2.correlate_batched(xd, mf, zc_v2.OFS_ZC_V2, want_mag=True, method=method)
+    assert torch.equal(got_c, want_c) and torch.equal(got_m, want_m)
+    got_d = zc_v2.detect_zc_preamble_batched(xd, mf)
+    assert torch.equal(got_d.n_events, want_d.n_events) and int(got_d.n_events[1]) >= 1
+    k = int(want_d.n_events[1])
+    assert torch.equal(got_d.events[1, :k], want_d.events[1, :k])
+    assert torch.equal(mf.correlate(xd, want_mag=True, method=method)[1], want_m)
 
 
 def test_zc_fft_plan_shared_by_two_streams():

@@ -152,3 +152,92 @@ def test_rtl_segment_parallel_iir_is_exact(shift, T, variant):
     s = O.minn_rtl_metric(xc, Q, shift, 3276, 15)
     for k in RTL_KEYS:
         assert np.array_equal(getattr(a, k)[1].cpu().numpy(), s[k]), k
+
+
+def _rtl_check_every_stream(iq, Q, variant, shift, hyst=2, toff=0, mode="float"):
+    """Exact kernel vs the general engine (EXACT=0, sequential recursion) AND the C oracle
+    (oracle_c.minn_rtl: minn_rtl.py:583-825 restated statement for statement) on EVERY stream,
+    every array bit for bit, every event."""
+    import oracle_c
+    xt = torch.from_numpy(iq).cuda()
+    kw = dict(smooth_shift=shift, threshold_value=3276, threshold_frac_bits=15, smooth_mode=mode,
+              hysteresis=hyst, timing_offset=toff)
+    a = _rtl_run(xt, Q, variant, True, **kw)
+    g = _rtl_run(xt, Q, variant, False, **kw)
+    for k in RTL_KEYS + ("n_events", "open_gate_start"):
+        assert torch.equal(getattr(a, k), getattr(g, k)), k
+    n = a.n_events.cpu().numpy()
+    for b in range(iq.shape[0]):
+        m = min(int(n[b]), a.events.shape[1])
+        assert torch.equal(a.events[b, :m], g.events[b, :m]), b
+    if mode != "float":
+        return a
+    xc = (iq[..., 0] + 1j * iq[..., 1]).astype(np.complex128)
+    o = oracle_c.minn_rtl(xc, Q, shift, 3276, 15, hyst, toff, max_events=int(a.events.shape[1]), nthreads=8)
+    for k in ("corr_total", "corr_positive", "smooth_metric", "energy_total", "corr_scaled", "energy_scaled"):
+        assert np.array_equal(getattr(a, k).cpu().numpy(), o[k]), k
+    assert np.array_equal(a.metric_valid.cpu().numpy(), o["metric_valid"].astype(bool))
+    assert np.array_equal(a.above_threshold.cpu().numpy(), o["above_threshold"].astype(bool))
+    assert np.array_equal(n, o["n_events"])
+    ev = a.events.cpu().numpy()
+    for b in range(iq.shape[0]):
+        k = min(int(n[b]), ev.shape[1])
+        assert np.array_equal(ev[b, :k], o["events"][b, :k]), b
+    return a
+
+
+@pytest.mark.parametrize("shift", [9, 12, 14, 15])
+@pytest.mark.parametrize("T", [1024, 2100, 4096])
+def test_rtl_fast_iir_slow_contraction_every_stream(shift, T, variant):
+    """Shifts 9-14 take the fma fast path of the segment-parallel IIR (aa_exact.hip, `interior`),
+    where the speculation chain contracts slowest per chunk (keep = 1 - 2^-shift) and needs the most
+    rounds; 15 is the first shift past it (the per-sample-select path).  minn_rtl.py:704-722."""
+    rng = np.random.default_rng(1000 + 7 * shift + T)
+    B, nb, Q = 12, 2, 64
+    iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q)))
+    a = _rtl_check_every_stream(iq, Q, variant, shift)
+    sm = a.smooth_metric.cpu().numpy()
+    assert (sm[:, -1] > 0).all()                       # the state is live through every segment
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_rtl_fast_iir_long_decay_through_guard(shift, variant):
+    """A burst followed by an all-zero tail: corr_positive is exactly 0 after the window passes,
+    so the IIR state decays by (1 - 2^-shift) per sample through the 2^-700 guard of the fast path
+    (aa_exact.hip `fast`) into the subnormal range and to 0.  Every stream bit for bit."""
+    rng = np.random.default_rng(40 + shift)
+    B, nb, Q, T = 8, 1, 64, 8192
+    x = np.zeros((B, nb, T), np.complex128)
+    for b in range(B):
+        s = int(rng.integers(0, 300))
+        blk = rng.normal(0, 500, Q) + 1j * rng.normal(0, 500, Q)
+        x[b, 0, :s] = rng.normal(0, 40, s) + 1j * rng.normal(0, 40, s)
+        x[b, 0, s:s + 4 * Q] = np.concatenate([blk, blk, -blk, -blk])
+    re = np.clip(np.round(x.real), -2048, 2047)
+    im = np.clip(np.round(x.imag), -2048, 2047)
+    iq = np.stack([re, im], axis=-1).astype(np.int16)
+    a = _rtl_check_every_stream(iq, Q, variant, shift)
+    sm = a.smooth_metric.cpu().numpy()
+    tiny = (sm > 0) & (sm < 2.0 ** -700)
+    assert tiny.any(axis=1).all()                      # every stream passes below the guard
+    assert (sm[:, -1] < 2.0 ** -1000).all()               # into the subnormal range
+
+
+@pytest.mark.parametrize("nb,Q", [(1, 64), (1, 256), (2, 64), (2, 256), (1, 128)])
+def test_rtl_exact_full_range_int16_after_int12_rows(nb, Q, variant):
+    """int16 words beyond 12 bits (+-30000) arriving after rows of 12-bit words: the int32 row-scan
+    path (aa_exact.hip IROW, nb = 1, E = 1 / 2) must switch to the fp64 scan at the first wide row
+    and carry the integer prefix across the switch.  Every stream bit for bit vs EXACT=0 and the
+    C oracle, in both IIR modes."""
+    rng = np.random.default_rng(500 + nb * Q)
+    B, T = 10, 3000
+    iq = _int12_bursts(rng, B, nb, T, ([1, 1, -1, -1], np.zeros(Q))).astype(np.int32)
+    for b in range(B):
+        s = 64 * int(rng.integers(1, 20)) + int(rng.integers(0, 64)) * (b % 2)   # wide from some row on
+        n = int(rng.integers(8, 600))
+        iq[b, :, s:s + n] = rng.integers(-30000, 30001, (nb, n, 2))
+        if b % 3 == 0:
+            iq[b, :, s + n + 500:] = rng.choice([-32768, 32767], (nb, T - s - n - 500, 2)) if T > s + n + 500 else 0
+    iq = iq.astype(np.int16)
+    _rtl_check_every_stream(iq, Q, variant, 3)
+    _rtl_check_every_stream(iq, Q, variant, 3, mode="floor")

@@ -76,6 +76,7 @@ def test_detector_recovers_drawn_cfo_and_offset():
     x0 = synth.synth_batch(base, 8, 1024 + 128, max_offset=0, snr_db=(30.0, 30.0), cfo_hz=(-4000.0, 4000.0),
                            fs=fs, seed=10)
     o0 = sync_aa.aa_detect_streaming_batched(x0, L=L)
+    assert bool((o0.n_events >= 1).all())                   # slot 0 is stored (slots past n_events are not)
     peak = o0.ev_int[:, 0, 0].cpu().numpy()
     assert np.max(np.abs(peak - (2 * L - 1))) <= 2
 

@@ -16,6 +16,8 @@ sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 import torch  # noqa: E402
 
 from ofdm_sync_amd import _lib, synth  # noqa: E402
+if os.environ.get("OFS_LIB"):   # a tools/variants.py tuning build, named explicitly (not a product switch)
+    _lib.use_tuning_library(os.environ["OFS_LIB"])
 
 
 def main():

@@ -13,6 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 import bench_configs as BC  # noqa: E402
 from ofdm_sync_amd import _lib  # noqa: E402
+if os.environ.get("OFS_LIB"):   # a tools/variants.py tuning build, named explicitly (not a product switch)
+    _lib.use_tuning_library(os.environ["OFS_LIB"])
 
 PHASES = ["cfo (CP loads + 2 block sums)", "pilot window -> LDS", "pilot FFT", "LS + atan2 (1200 bins)",
           "unwrap + slope", "data window -> LDS", "data FFT", "EQ + gain sums", "gain, EVM, outputs"]

@@ -31,6 +31,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from ofdm_sync_amd import _lib, shard, synth, zc_freq  # noqa: E402
+if os.environ.get("OFS_LIB"):   # a tools/variants.py tuning build, named explicitly (not a product switch)
+    _lib.use_tuning_library(os.environ["OFS_LIB"])
 
 HBM = 8000.0
 VPEAK = {"fp32": 157.3, "fp64": 78.6}    # MI355X vector FMA peaks, TFLOP/s (spec; no MFMA: no contraction)

@@ -2,7 +2,8 @@
 recompiled per variant; the others are compiled once.  Diagnostic tooling (not the product).
 
     python tools/variants.py aa_fast.hip "pd2=-DOFS_STREAM_PD=2" "w4=-DOFS_STREAM_WAVES=4" ...
-Writes build/libofdmsync_<name>.so (source-hash check is skipped for OFS_LIB builds).
+Writes build/libofdmsync_<name>.so (load one with `OFS_LIB=... python tools/<tool>.py`: the tools pass it to
+_lib.use_tuning_library, which accepts only a library whose baked hash reads variant-<name>).
 """
 import concurrent.futures as cf
 import os

@@ -14,6 +14,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 import bench_configs as BC  # noqa: E402
 from ofdm_sync_amd import _lib  # noqa: E402
+if os.environ.get("OFS_LIB"):   # a tools/variants.py tuning build, named explicitly (not a product switch)
+    _lib.use_tuning_library(os.environ["OFS_LIB"])
 
 ROLES = ["walker: DMA issue + wait", "walker: chain", "walker: barrier", "helpers: work", "helpers: barrier"]
 
