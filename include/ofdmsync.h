@@ -92,6 +92,8 @@ const char* ofs_status_string(int32_t status);
  *   ZS_GBLK      0: Horner block DFTs in the pair kernel instead of Goertzel
  *   MC_FUSED     0: ZC matched filter through the rocFFT pipeline instead of the fused LDS FFT
  *   MC_FUSE_X    0: fused LDS FFT with the separate extract kernel
+ *   MC_PERS      0: fused LDS FFT one block per 1024-thread workgroup instead of the persistent
+ *                512-thread kernel that prefetches the next block
  *   ZC_SEQ       1: zc_v2 CFAR + gate through the sequential one-wave-per-stream kernel
  *   ZC_NODMA     1: zc_v2 CFAR tiles through registers instead of LDS-DMA
  *   BE_FAST      0: receiver back-end through the generic kernel
@@ -420,6 +422,17 @@ int32_t ofs_zc_fft_plan_create2(int32_t precision, int32_t N, int64_t n_windows,
 int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows, int64_t in_dist,
                                 int32_t prune_bins, int64_t chunk_windows, void** plan_out,
                                 size_t* work_bytes);
+/* ROWS plan for the reference's sliding shape (many offsets per stream): one rocFFT execution covers
+ * EVERY offset of rows_per_exec consecutive [T]-sample rows (rows = stream x branch; 0 = all
+ * total_rows; at execute time a multiple of n_br) - its windows start at sample cp of the first row
+ * at a distance of ONE sample, (rows-1)*T + n_off of them, and the store callback keeps the template
+ * bins of the windows that lie inside one row (always pruned: prune_bins = n_bins, N a power of two
+ * <= 4096).  ofs_zc_freq_metric_fft then issues 2 launches per row group instead of 2 per offset;
+ * the spectrum buffer is [ofs_zc_fft_plan_chunk(plan)][prune_bins].  The FFTs cover T instead of
+ * n_off windows per row (T / n_off times the per-offset plan's transforms). */
+int32_t ofs_zc_fft_plan_create_rows(int32_t precision, int32_t N, int32_t cp, int64_t T,
+                                    int64_t total_rows, int64_t rows_per_exec, int32_t prune_bins,
+                                    void** plan_out, size_t* work_bytes);
 int64_t ofs_zc_fft_plan_chunk(const void* plan);
 int32_t ofs_zc_fft_plan_destroy(void* plan);
 /*

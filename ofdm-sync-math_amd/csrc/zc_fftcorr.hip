@@ -38,6 +38,7 @@ struct McPlan {
     double2* H = nullptr;           // [M] FFT of the reversed conjugated reference
     double2* Hbr = nullptr;         // fused path (M = MF_M): H[bitrev(i)] / M, then 128 twiddles
     double ref_norm = 0.0;
+    int n_cu = 0;                   // persistent fused kernel: workgroups (one per CU), 0 = not set up
     size_t work_bytes = 0;
     size_t scratch_bytes = 0;
     rocfft_execution_info info = nullptr;   // reused by every call (stream / work buffer set per call)
@@ -451,6 +452,301 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
     }
 }
 
+// ---- persistent overlap-save kernel (M = 8192): one 512-thread workgroup per CU walks a contiguous run of
+// blocks and overlaps each block's HBM traffic with the neighbouring blocks' arithmetic ----
+// mc_fused_kernel runs one block per 1024-thread workgroup; its 141 KiB of LDS admit one workgroup per CU,
+// so a block's 128 KiB input load, its FFTs and its 147 KiB of output stores run one after another on
+// the CU (53 % of wave cycles waiting, 12.9 % VALU, profiles/r04d_*).  Here the next block's input is
+// loaded into registers during the current block's second half, and the current block's stores drain
+// during the next block's first half.  512 threads x 16 elements (2 waves per SIMD, up to 256 VGPRs):
+//   forward DIF  spans 4096..512 in registers (elements t + 512m)    | twiddle base w_8192^t
+//                spans  256..32  LDS pass, elements 512g + 32i + k    | base w_512^k  (g = t/32, k = t%32)
+//                spans   16..1   LDS pass, elements 16t + i, lane pairs (span 16 across the pair by DPP)
+//   conj(X * H / M) in bit-reversed order (Hbr, as mc_fused_kernel)
+//   inverse DIT  spans 1..16 (same pass), 32..256 (LDS pass), 512..4096 (registers)
+// 4 LDS passes instead of 5, each stage's twiddle one product with a per-thread base (bases from a
+// table built once per launch).  gfx9 counts loads and stores on one vmcnt and they complete out of
+// order, so waiting for any load waits for every store in flight: the Hbr slice is loaded right after
+// the previous block's stores (waited for in the middle pass, by when those stores have drained), and the
+// next block's input is taken into registers BEFORE this block's stores are issued.
+constexpr int MP_T = 512;
+constexpr int MP_LDS = (MF_M + 512 + 32) * 16 + 8 * 8;   // block, w_8192^t (t < 512), w_512^k (k < 32), wave sums
+// slot of block element e: low four bits XOR bits 4-7 (conflict-free for t + 512m, 512g + 32i + k, 16t + i)
+__device__ __forceinline__ int mp_at(int e) { return e ^ ((e >> 4) & 15); }
+// energy prefix P[j] (doubles, in the block region during the extract): one pad per 16
+__device__ __forceinline__ int mp_pq(int j) { return j + (j >> 4); }
+__device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+// v * e^{-i pi q / 16}, q < 16 known at compile time (the span-16 stage of the middle pass)
+__device__ __forceinline__ double2 mp_w32(double2 v, int q) {
+    if ((q & 1) == 0) return mf_w16(v, q >> 1);
+    constexpr double C[8] = {0.98078528040323044913, 0.83146961230254523708, 0.55557023301960222474,
+                             0.19509032201612826785, -0.19509032201612826785, -0.55557023301960222474,
+                             -0.83146961230254523708, -0.98078528040323044913};   // cos(pi q / 16), q odd
+    constexpr double S[8] = {0.19509032201612826785, 0.55557023301960222474, 0.83146961230254523708,
+                             0.98078528040323044913, 0.98078528040323044913, 0.83146961230254523708,
+                             0.55557023301960222474, 0.19509032201612826785};     // sin(pi q / 16)
+    const double c = C[q >> 1], s = S[q >> 1];
+    return make_double2(fma(v.x, c, v.y * s), fma(v.y, c, -(v.x * s)));
+}
+// 16-point radix-2 DIF over v[0..15] (spans 8, 4, 2, 1 in units of the caller's stride) with twiddles
+// base^{j} * w16^{...}: span 8 pairs (m, m+8) take b * w16^m, span 4 b^2 * w16^{2(m%4)}, span 2
+// b^4 * w16^{4(m%2)}, span 1 b^8.  UNIT: base 1 (no products with b).
+template <bool UNIT>
+__device__ __forceinline__ void mp_dif16(double2 (&v)[16], double2 b) {
+    double2 b2 = b, b4 = b, b8 = b;
+    if (!UNIT) { b2 = mf_mul(b, b); b4 = mf_mul(b2, b2); b8 = mf_mul(b4, b4); }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const double2 a = v[m], c = v[m + 8];
+        v[m] = c_add(a, c);
+        v[m + 8] = mf_w16(UNIT ? c_sub(a, c) : mf_mul(c_sub(a, c), b), m);
+    }
+#pragma unroll
+    for (int h = 0; h < 16; h += 8)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 a = v[h + m], c = v[h + m + 4];
+            v[h + m] = c_add(a, c);
+            v[h + m + 4] = mf_w16(UNIT ? c_sub(a, c) : mf_mul(c_sub(a, c), b2), 2 * m);
+        }
+#pragma unroll
+    for (int h = 0; h < 16; h += 4)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const double2 a = v[h + m], c = v[h + m + 2];
+            v[h + m] = c_add(a, c);
+            v[h + m + 2] = mf_w16(UNIT ? c_sub(a, c) : mf_mul(c_sub(a, c), b4), 4 * m);
+        }
+#pragma unroll
+    for (int m = 0; m < 16; m += 2) {
+        const double2 a = v[m], c = v[m + 1];
+        v[m] = c_add(a, c);
+        v[m + 1] = UNIT ? c_sub(a, c) : mf_mul(c_sub(a, c), b8);
+    }
+}
+// the matching radix-2 DIT (spans 1, 2, 4, 8): bit-reversed in, natural out
+template <bool UNIT>
+__device__ __forceinline__ void mp_dit16(double2 (&v)[16], double2 b) {
+    double2 b2 = b, b4 = b, b8 = b;
+    if (!UNIT) { b2 = mf_mul(b, b); b4 = mf_mul(b2, b2); b8 = mf_mul(b4, b4); }
+#pragma unroll
+    for (int m = 0; m < 16; m += 2) {
+        const double2 u = v[m], w = UNIT ? v[m + 1] : mf_mul(v[m + 1], b8);
+        v[m] = c_add(u, w);
+        v[m + 1] = c_sub(u, w);
+    }
+#pragma unroll
+    for (int h = 0; h < 16; h += 4)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const double2 u = v[h + m], w = mf_w16(UNIT ? v[h + m + 2] : mf_mul(v[h + m + 2], b4), 4 * m);
+            v[h + m] = c_add(u, w);
+            v[h + m + 2] = c_sub(u, w);
+        }
+#pragma unroll
+    for (int h = 0; h < 16; h += 8)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const double2 u = v[h + m], w = mf_w16(UNIT ? v[h + m + 4] : mf_mul(v[h + m + 4], b2), 2 * m);
+            v[h + m] = c_add(u, w);
+            v[h + m + 4] = c_sub(u, w);
+        }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const double2 u = v[m], w = mf_w16(UNIT ? v[m + 8] : mf_mul(v[m + 8], b), m);
+        v[m] = c_add(u, w);
+        v[m + 8] = c_sub(u, w);
+    }
+}
+
+template <int FMT>
+__device__ __forceinline__ void mp_load(const McArgs& a, int64_t blk, int t, double2 (&d)[16]) {
+    const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+    const int64_t g0 = q * a.S - (a.N - 1) + t;
+    const int64_t base = row * a.T;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int64_t g = g0 + MP_T * m;
+        d[m] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, base + g) : make_double2(0.0, 0.0);
+    }
+}
+
+template <int FMT, bool FUSE_X>
+__global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* __restrict__ Hbr, int64_t total) {
+    extern __shared__ __attribute__((aligned(16))) double2 fb[];    // [MF_M] block, tb[512], tc[32], wave sums
+    double2* tb = fb + MF_M;
+    double2* tc = tb + MP_T;
+    double* wsum = reinterpret_cast<double*>(tc + 32);
+    const int t0 = threadIdx.x, lane = t0 & 63, wv = t0 >> 6;
+    {                                                               // twiddle bases, once per launch
+        double sn, cs;
+        sincospi(-2.0 * (double)t0 / (double)MF_M, &sn, &cs);
+        tb[t0] = make_double2(cs, sn);                                // w_8192^t
+        if (t0 < 32) {
+            sincospi(-2.0 * (double)t0 / 512.0, &sn, &cs);
+            tc[t0] = make_double2(cs, sn);                            // w_512^k
+        }
+    }
+    const int64_t G = gridDim.x, wg = blockIdx.x;
+    const int64_t b0 = wg * total / G, b1 = (wg + 1) * total / G;   // this workgroup's run of blocks
+    if (b0 >= b1) return;                                           // (whole workgroup)
+    double2 v[16];
+    double en[FUSE_X ? 16 : 1];                                     // |u|^2 of this block's samples t + 512m
+    mp_load<FMT>(a, b0, t0, v);
+    if constexpr (FUSE_X) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) en[m] = fma(v[m].x, v[m].x, v[m].y * v[m].y);
+    }
+    for (int64_t blk = b0; blk < b1; ++blk) {
+        const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+        // the thread index re-materialised per block (opaque to the optimiser): the per-thread LDS
+        // addresses, twiddle bases and the H slice are loop-invariant, and hoisting them out of the block
+        // loop would pin ~100 VGPRs for the whole launch
+        int t = t0;
+        asm volatile("" : "+v"(t));
+        const int g2 = t >> 5, k2 = t & 31;                          // LDS pass position: 512 g2 + 32 i + k2
+        // ---- forward: spans 4096..512 in registers ----
+        mp_dif16<false>(v, tb[t]);
+        mf_sync();                                                  // previous block's LDS readers done
+#pragma unroll
+        for (int m = 0; m < 16; ++m) fb[mp_at(t + MP_T * m)] = v[m];
+        mf_sync();
+        // ---- spans 256..32 ----
+        {
+            const int p = 512 * g2 + k2;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = fb[mp_at(p + 32 * i)];
+            mp_dif16<false>(v, tc[k2]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fb[mp_at(p + 32 * i)] = v[i];
+        }
+        mf_sync();
+        // ---- spans 16..1, conj(X H / M), spans 1..16: lane pair (t, t^1) holds elements 32(t/2) .. +31 ----
+        {
+            const bool hi = (t & 1) != 0;
+            // this block's H slice (L2-resident): waiting for it also waits for the previous block's stores
+            // (one vmcnt), which have had the first two passes to drain
+            double2 hb[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) hb[i] = Hbr[16 * t + i];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = fb[mp_at(16 * t + i)];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {                          // DIF span 16 across the pair
+                const double2 o = mf_swap_pair(v[i]);
+                const double2 x0 = hi ? o : v[i], x1 = hi ? v[i] : o;
+                v[i] = hi ? mp_w32(c_sub(x0, x1), i) : c_add(x0, x1);
+            }
+            mp_dif16<true>(v, make_double2(1.0, 0.0));
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const double2 y = mf_mul(v[i], hb[i]);
+                v[i] = make_double2(y.x, -y.y);
+            }
+            mp_dit16<true>(v, make_double2(1.0, 0.0));
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {                          // DIT span 16 across the pair
+                const double2 o = mf_swap_pair(v[i]);
+                const double2 u = hi ? o : v[i], w = mp_w32(hi ? v[i] : o, i);
+                v[i] = hi ? c_sub(u, w) : c_add(u, w);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fb[mp_at(16 * t + i)] = v[i];
+        }
+        mf_sync();
+        // the next block's input: in flight through the second half of this block
+        const bool more = blk + 1 < b1;
+        double2 nx[16];
+        if (more) {
+            mp_load<FMT>(a, blk + 1, t, nx);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) nx[m] = make_double2(0.0, 0.0);
+        }
+        // ---- inverse spans 32..256 ----
+        {
+            const int p = 512 * g2 + k2;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = fb[mp_at(p + 32 * i)];
+            mp_dit16<false>(v, tc[k2]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) fb[mp_at(p + 32 * i)] = v[i];
+        }
+        mf_sync();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = fb[mp_at(t + MP_T * m)];
+        mp_dit16<false>(v, tb[t]);                                  // spans 512..4096: natural order out
+        const int64_t n0 = q * a.S;
+        const int ns = (int)min((int64_t)a.S, a.nout - n0);
+        if constexpr (!FUSE_X) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) { const double2 w = v[m]; v[m] = nx[m]; nx[m] = w; }   // next input in
+            __builtin_amdgcn_sched_barrier(0);                      // ... before this block's stores
+            double2* dst = a.U + blk * (int64_t)MF_M;
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int o = t + MP_T * m;
+                if (o >= a.N - 1) dst[o] = make_double2(nx[m].x, -nx[m].y);
+            }
+            continue;
+        }
+        // ---- fused extract (one branch): window energies from an fp64 prefix of |u|^2 in the block LDS ----
+        // P[j] = sum_{i<j} |u_i|^2 in place of |u_j|^2 (each thread rewrites only the 16 slots it read, so
+        // no neighbour's input is overwritten), P[M] at slot mp_pq(M)
+        mf_sync();                                                  // every thread has read its block slots
+        double* P = reinterpret_cast<double*>(fb);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) P[mp_pq(t + MP_T * m)] = en[m];
+        mf_sync();
+        double loc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) loc += P[mp_pq(16 * t + i)];
+        const double incl = ofs::wave_scan_add(loc, lane);
+        if (lane == 63) wsum[wv] = incl;
+        mf_sync();                                                  // (LDS re-read below: the fence)
+        double run = incl - loc;
+        for (int k = 0; k < wv; ++k) run += wsum[k];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int j = mp_pq(16 * t + i);
+            const double e = P[j];
+            P[j] = run;
+            run += e;
+        }
+        if (t == MP_T - 1) P[mp_pq(MF_M)] = run;
+        // next block's input taken into registers (and its energies) before any store of this block issues
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const double2 w = v[m];
+            v[m] = nx[m];
+            nx[m] = w;
+            en[m] = fma(v[m].x, v[m].x, v[m].y * v[m].y);
+        }
+        mf_sync();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const int o = t + MP_T * m, s = o - (a.N - 1);
+            if (s < 0 || s >= ns) continue;
+            const double2 c = make_double2(nx[m].x, -nx[m].y);
+            const int64_t oi = row * a.nout + n0 + s;               // one branch: row = stream
+            if (a.mode == OFS_ZC_RAW || a.mode == OFS_ZC_SUM) {
+                if (a.out) a.out[oi] = c;
+                if (a.mag) a.mag[oi] = sqrt(fma(c.x, c.x, c.y * c.y));
+                continue;
+            }
+            const double e = P[mp_pq(o + 1)] - P[mp_pq(o + 1 - a.N)];   // sum |x|^2 over the N-sample window
+            const double ewc = a.mode == OFS_ZC_V2 ? (e > 1e-12 ? e : 1e-12)                 // zc_v2.py:268
+                                                   : (e > 0.0 ? e : 0.0) + 1e-12;            // zc.py:113-126
+            const double inv = 1.0 / (a.ref_norm * sqrt(ewc));
+            const double2 r = make_double2(c.x * inv, c.y * inv);
+            if (a.out) a.out[oi] = r;
+            if (a.mag) a.mag[oi] = sqrt(fma(r.x, r.x, r.y * r.y));
+        }
+    }
+}
+
 // Hbr[i] = H[bitrev(i)] / M, for the fused path; then the kernel's two 64-entry twiddle tables
 // Hbr[M + l] = w^l, Hbr[M + 64 + h] = w^{64h} (from sincospi of exact ratios, once per plan)
 __global__ void mc_prep_kernel(const double2* H, double2* Hbr, int M, int lb) {
@@ -667,6 +963,18 @@ int32_t ofs_zc_mf_plan_create(const void* ref, int32_t N, int64_t B, int32_t n_b
             if (!okf) {
                 (void)hipFree(p->Hbr);
                 p->Hbr = nullptr;
+            } else {
+                int dev = 0, ncu = 0;
+                const int pl = MP_LDS;
+                if (hipGetDevice(&dev) == hipSuccess &&
+                    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_C64, false>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_C128, false>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_CI16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_C64, true>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_C128, true>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess &&
+                    hipFuncSetAttribute((const void*)mc_pers_kernel<OFS_CI16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, pl) == hipSuccess)
+                    p->n_cu = ncu > 0 ? ncu : 0;
             }
         } else {
             p->Hbr = nullptr;
@@ -715,8 +1023,14 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
         const dim3 gf((unsigned)(rows * p->nblk));
         const size_t fl = MF_LDS;
         const bool fx = n_br == 1 && mc_fuse_extract();             // one branch: no scratch round trip
+        const int64_t total = rows * p->nblk;
+        const bool pers = p->n_cu > 0 && !ofs::variant_off(ofs::V_MC_PERS);
+        const dim3 gpers((unsigned)std::min<int64_t>(total, p->n_cu));
+        const size_t pl = MP_LDS;
 #define MF_GO(F)                                                                                      \
-        if (fx) hipLaunchKernelGGL((mc_fused_kernel<F, true>), gf, dim3(MF_T), fl, st, a, p->Hbr);     \
+        if (pers && fx) hipLaunchKernelGGL((mc_pers_kernel<F, true>), gpers, dim3(MP_T), pl, st, a, p->Hbr, total); \
+        else if (pers) hipLaunchKernelGGL((mc_pers_kernel<F, false>), gpers, dim3(MP_T), pl, st, a, p->Hbr, total); \
+        else if (fx) hipLaunchKernelGGL((mc_fused_kernel<F, true>), gf, dim3(MF_T), fl, st, a, p->Hbr);     \
         else hipLaunchKernelGGL((mc_fused_kernel<F, false>), gf, dim3(MF_T), fl, st, a, p->Hbr);
         switch (in_fmt) {
             case OFS_C64: MF_GO(OFS_C64) break;

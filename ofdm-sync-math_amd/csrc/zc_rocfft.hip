@@ -32,22 +32,28 @@ constexpr int ZWG = 256;        // 4 waves = 4 streams per workgroup
 struct ZcCbData {
     void* compact;              // [n_windows][n_bins] c64 | c128
     int32_t n_bins, log2N;
+    int64_t row_T, n_off;       // rows plans: windows w with w % row_T >= n_off straddle two rows (dropped)
     int16_t slot[4096];
 };
 
+__device__ __forceinline__ bool zc_cb_keep(const ZcCbData* d, size_t w) {
+    return d->row_T == 0 || (int64_t)(w % (size_t)d->row_T) < d->n_off;
+}
 __device__ void zc_store_cb_f32(void* data, size_t offset, float2 element, void* cbdata, void*) {
     (void)data;
     const ZcCbData* d = static_cast<const ZcCbData*>(cbdata);
     const size_t k = offset & ((size_t(1) << d->log2N) - 1);
     const int s = d->slot[k];
-    if (s >= 0) static_cast<float2*>(d->compact)[(offset >> d->log2N) * d->n_bins + s] = element;
+    const size_t w = offset >> d->log2N;
+    if (s >= 0 && zc_cb_keep(d, w)) static_cast<float2*>(d->compact)[w * d->n_bins + s] = element;
 }
 __device__ void zc_store_cb_f64(void* data, size_t offset, double2 element, void* cbdata, void*) {
     (void)data;
     const ZcCbData* d = static_cast<const ZcCbData*>(cbdata);
     const size_t k = offset & ((size_t(1) << d->log2N) - 1);
     const int s = d->slot[k];
-    if (s >= 0) static_cast<double2*>(d->compact)[(offset >> d->log2N) * d->n_bins + s] = element;
+    const size_t w = offset >> d->log2N;
+    if (s >= 0 && zc_cb_keep(d, w)) static_cast<double2*>(d->compact)[w * d->n_bins + s] = element;
 }
 __device__ void* zc_store_cb_f32_ptr = (void*)zc_store_cb_f32;
 __device__ void* zc_store_cb_f64_ptr = (void*)zc_store_cb_f64;
@@ -65,6 +71,11 @@ struct ZcFftPlan {
     ZcCbData* cb_dev = nullptr; // device copy of the callback data
     ZcCbData* cb_host = nullptr;// pinned staging
     void* cb_fn = nullptr;      // device address of the store callback
+    // rows plan (ofs_zc_fft_plan_create_rows): every offset of `rows` consecutive [T]-sample rows in ONE
+    // execution - windows at distance 1 sample from sample cp of the first row
+    int64_t rows = 0;           // rows per execution (0: the per-offset plan above)
+    int64_t row_T = 0, n_off = 0;
+    int32_t cp = 0;
 };
 
 struct GatherArgs {
@@ -112,6 +123,43 @@ __global__ __launch_bounds__(ZWG) void zc_gather_kernel(GatherArgs a) {
         const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
         if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[(a.b0 + b) * a.n_off + a.off] = (float)v;
         else reinterpret_cast<double*>(a.metric)[(a.b0 + b) * a.n_off + a.off] = v;
+    }
+}
+
+// rows plans: metric[b][off] for every offset of the execution's streams from the compact spectrum of
+// windows w = (b·n_br + br)·T + off.  One wave per (stream, offset), lane k = template bin k.
+template <class R>
+__global__ __launch_bounds__(ZWG) void zc_gather_rows_kernel(GatherArgs a, int64_t T) {
+    const int lane = threadIdx.x & 63;
+    const int64_t off = (int64_t)blockIdx.x * (ZWG / 64) + (threadIdx.x >> 6), b = blockIdx.y;
+    if (off >= a.n_off) return;
+    double cr = 0.0, ci = 0.0, en = 0.0;
+    if (lane < a.n_bins) {
+        const double tr = a.t_re[lane], ti = a.t_im[lane];
+        for (int br = 0; br < a.n_br; ++br) {
+            const int64_t i = ((b * a.n_br + br) * T + off) * a.n_bins + lane;
+            double xr, xi;
+            if constexpr (sizeof(R) == 4) {
+                const float2 v = reinterpret_cast<const float2*>(a.spec)[i];
+                xr = v.x; xi = v.y;
+            } else {
+                const double2 v = reinterpret_cast<const double2*>(a.spec)[i];
+                xr = v.x; xi = v.y;
+            }
+            cr += tr * xr + ti * xi;                     // conj(t) * x   (zc_freq.py:88-95)
+            ci += tr * xi - ti * xr;
+            en += xr * xr + xi * xi;
+        }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        cr += __shfl_xor(cr, m);
+        ci += __shfl_xor(ci, m);
+        en += __shfl_xor(en, m);
+    }
+    if (lane == 0) {
+        const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
+        if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[(a.b0 + b) * a.n_off + off] = (float)v;
+        else reinterpret_cast<double*>(a.metric)[(a.b0 + b) * a.n_off + off] = v;
     }
 }
 
@@ -261,6 +309,58 @@ int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows,
     return OFS_OK;
 }
 
+int32_t ofs_zc_fft_plan_create_rows(int32_t precision, int32_t N, int32_t cp, int64_t T, int64_t total_rows,
+                                    int64_t rows_per_exec, int32_t prune_bins, void** plan_out, size_t* work_bytes) {
+    if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || cp < 0 || total_rows < 1 ||
+        rows_per_exec < 0 || prune_bins < 1 || prune_bins > ZB || N > 4096 || (N & (N - 1)))
+        return OFS_EINVAL;
+    if (T < (int64_t)N + cp) return OFS_ESHORT;
+    *plan_out = nullptr;
+    std::call_once(g_setup, [] { rocfft_setup(); });
+    ZcFftPlan* p = new ZcFftPlan;
+    p->rows = (rows_per_exec == 0 || rows_per_exec > total_rows) ? total_rows : rows_per_exec;
+    p->row_T = T;
+    p->n_off = T - ((int64_t)N + cp) + 1;
+    p->cp = cp;
+    auto wins = [&](int64_t r) { return (r - 1) * T + p->n_off; };  // windows covering r rows' offsets
+    p->chunk = wins(p->rows);
+    rocfft_status s = make_fft_plan(precision, N, p->chunk, 1, &p->plan);
+    if (s == rocfft_status_success && total_rows % p->rows)
+        s = make_fft_plan(precision, N, wins(total_rows % p->rows), 1, &p->tail);
+    size_t wb = 0;
+    if (s == rocfft_status_success) s = rocfft_plan_get_work_buffer_size(p->plan, &p->work_bytes);
+    if (s == rocfft_status_success && p->tail) s = rocfft_plan_get_work_buffer_size(p->tail, &wb);
+    if (s != rocfft_status_success) {
+        if (p->plan) rocfft_plan_destroy(p->plan);
+        if (p->tail) rocfft_plan_destroy(p->tail);
+        delete p;
+        return OFS_EFFT;
+    }
+    if (wb > p->work_bytes) p->work_bytes = wb;
+    p->precision = precision;
+    p->N = N;
+    p->n_windows = total_rows;
+    p->in_dist = T;
+    p->prune = prune_bins;
+    bool ok = hipMalloc(&p->cb_dev, sizeof(ZcCbData)) == hipSuccess &&
+              hipHostMalloc(&p->cb_host, sizeof(ZcCbData)) == hipSuccess &&
+              (memset(p->cb_host, 0, sizeof(ZcCbData)), true) &&
+              hipMemcpyFromSymbol(&p->cb_fn, precision == OFS_FP32 ? HIP_SYMBOL(zc_store_cb_f32_ptr)
+                                                                  : HIP_SYMBOL(zc_store_cb_f64_ptr),
+                                  sizeof(void*)) == hipSuccess && p->cb_fn;
+    if (!ok) {
+        if (p->cb_dev) (void)hipFree(p->cb_dev);
+        if (p->cb_host) (void)hipHostFree(p->cb_host);
+        rocfft_plan_destroy(p->plan);
+        if (p->tail) rocfft_plan_destroy(p->tail);
+        delete p;
+        return OFS_EHIP;
+    }
+    if (work_bytes) *work_bytes = p->work_bytes;
+    *plan_out = p;
+    return OFS_OK;
+}
+
 int64_t ofs_zc_fft_plan_chunk(const void* plan) {
     const ZcFftPlan* p = static_cast<const ZcFftPlan*>(plan);
     return p ? p->chunk : 0;
@@ -287,6 +387,7 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
         return OFS_EINVAL;
     const int32_t want_fmt = p->precision == OFS_FP32 ? OFS_C64 : OFS_C128;
     if (in_fmt != want_fmt || p->N != N || p->in_dist != T || p->n_windows != B * (int64_t)n_br) return OFS_EINVAL;
+    if (p->rows && (p->cp != cp || p->rows % n_br)) return OFS_EINVAL;
     if (p->work_bytes && !work) return OFS_EINVAL;
     if (p->prune && p->prune != n_bins) return OFS_EINVAL;
     if (T < (int64_t)N + cp) return OFS_ESHORT;
@@ -314,6 +415,8 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
         ZcCbData h{};
         h.compact = spectrum;
         h.n_bins = n_bins;
+        h.row_T = p->rows ? T : 0;
+        h.n_off = p->rows ? n_off : 0;
         while ((1 << h.log2N) < N) ++h.log2N;
         for (int k = 0; k < 4096; ++k) h.slot[k] = -1;
         for (int k = 0; k < n_bins; ++k) {
@@ -341,10 +444,41 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
         s = rocfft_execution_info_set_store_callback(info, fns, dat, 0);
     }
     const size_t esz = p->precision == OFS_FP32 ? 8 : 16;
-    const unsigned grid = (unsigned)((B + ZWG / 64 - 1) / (ZWG / 64));
-    if (p->chunk % n_br) { rocfft_execution_info_destroy(info); return OFS_EINVAL; }
-    const int64_t cs = p->chunk / n_br;             // streams per rocFFT execution
     int32_t rc = OFS_OK;
+    if (p->rows) {
+        // rows plan: ONE execution per `rows` rows covers every offset of them (windows at distance one
+        // sample, the ones straddling two rows dropped by the callback), then one gather over
+        // (stream, offset): 2 launches per row group instead of 2 per offset
+        const int64_t total = B * (int64_t)n_br;
+        for (int64_t r0 = 0; r0 < total && s == rocfft_status_success && rc == OFS_OK; r0 += p->rows) {
+            const int64_t nr = total - r0 < p->rows ? total - r0 : p->rows;
+            void* in[1] = {const_cast<char*>(static_cast<const char*>(x)) + ((size_t)r0 * T + (size_t)cp) * esz};
+            void* out[1] = {spectrum};
+            s = rocfft_execute(nr == p->rows ? p->plan : p->tail, in, out, info);
+            if (s != rocfft_status_success) break;
+            g.b0 = r0 / n_br;
+            g.B = nr / n_br;
+            const dim3 gr((unsigned)((n_off + ZWG / 64 - 1) / (ZWG / 64)), (unsigned)g.B);
+            if (p->precision == OFS_FP32) hipLaunchKernelGGL(zc_gather_rows_kernel<float>, gr, dim3(ZWG), 0, st, g, T);
+            else hipLaunchKernelGGL(zc_gather_rows_kernel<double>, gr, dim3(ZWG), 0, st, g, T);
+            if (hipGetLastError() != hipSuccess) rc = OFS_EHIP;
+        }
+    }
+    if (p->rows || p->chunk % n_br) {
+        rocfft_execution_info_destroy(info);
+        if (!p->rows) return OFS_EINVAL;
+        if (s != rocfft_status_success) return OFS_EFFT;
+        if (rc) return rc;
+        if (peak_index || peak_value) {
+            if (p->precision == OFS_FP32)
+                launch_argmax(static_cast<const float*>(metric), B, n_off, peak_index, peak_value, st);
+            else
+                launch_argmax(static_cast<const double*>(metric), B, n_off, peak_index, peak_value, st);
+            if (hipGetLastError() != hipSuccess) return OFS_EHIP;
+        }
+        return OFS_OK;
+    }
+    const int64_t cs = p->chunk / n_br;             // streams per rocFFT execution
     // windows x[b][br][off+cp : off+cp+N], distance T: one batched transform per chunk of streams
     // and offset.  A chunked plan reuses one [chunk][N] spectrum buffer small enough to stay in the
     // Infinity Cache between the FFT's store and the gather's read, and walks a chunk's offsets

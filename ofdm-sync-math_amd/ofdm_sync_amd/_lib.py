@@ -117,6 +117,8 @@ def _declare(lib):
                                               ctypes.POINTER(ctypes.c_size_t)]),
         "ofs_zc_fft_plan_create3": (c_int32, [c_int32, c_int32, c_int64, c_int64, c_int32, c_int64, P,
                                               ctypes.POINTER(ctypes.c_size_t)]),
+        "ofs_zc_fft_plan_create_rows": (c_int32, [c_int32, c_int32, c_int32, c_int64, c_int64, c_int64, c_int32, P,
+                                                  ctypes.POINTER(ctypes.c_size_t)]),
         "ofs_zc_fft_plan_chunk": (c_int64, [P]),
         "ofs_zc_fft_plan_destroy": (c_int32, [P]),
         "ofs_zc_freq_metric_fft": (c_int32, [P, c_int32, P, c_int64, c_int32, c_int64, c_int32, c_int32,

@@ -115,18 +115,27 @@ class FFTPlan:
     spectrum buffer is then [chunk][prune_bins]).  ``chunk`` windows per rocFFT execution (0: all
     of them); ``self.chunk`` is the spectrum buffer's row count."""
 
-    def __init__(self, precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0):
+    def __init__(self, precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0,
+                 rows_cp: int | None = None):
+        """rows_cp not None: a ROWS plan (ofs_zc_fft_plan_create_rows) over n_windows = B * n_branch rows
+        of T samples, cp = rows_cp, ``chunk`` rows per execution; every offset of a row group is one
+        execution (windows one sample apart), pruned to ``prune_bins`` bins."""
         import ctypes
         self._lib = _lib.lib()
         h = ctypes.c_void_p()
         wb = ctypes.c_size_t()
-        _lib.check(self._lib.ofs_zc_fft_plan_create3(int(precision), int(N), int(n_windows), int(T), int(prune_bins),
-                                                    int(chunk), ctypes.byref(h), ctypes.byref(wb)),
-                   "ofs_zc_fft_plan_create3")
+        if rows_cp is None:
+            _lib.check(self._lib.ofs_zc_fft_plan_create3(int(precision), int(N), int(n_windows), int(T),
+                                                        int(prune_bins), int(chunk), ctypes.byref(h), ctypes.byref(wb)),
+                       "ofs_zc_fft_plan_create3")
+        else:
+            _lib.check(self._lib.ofs_zc_fft_plan_create_rows(int(precision), int(N), int(rows_cp), int(T), int(n_windows),
+                                                            int(chunk), int(prune_bins), ctypes.byref(h),
+                                                            ctypes.byref(wb)), "ofs_zc_fft_plan_create_rows")
         self.handle, self.work_bytes = h.value, int(wb.value)
         self.prune_bins = int(prune_bins)
         self.chunk = int(self._lib.ofs_zc_fft_plan_chunk(self.handle))
-        self.key = (int(precision), int(N), int(n_windows), int(T), int(prune_bins), int(chunk))
+        self.key = (int(precision), int(N), int(n_windows), int(T), int(prune_bins), int(chunk), rows_cp)
 
     def __del__(self):
         h, self.handle = getattr(self, "handle", None), None
@@ -137,14 +146,25 @@ class FFTPlan:
 _plans: dict = {}
 
 
-def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0) -> FFTPlan:
-    key = (precision, N, n_windows, T, prune_bins, chunk)
+def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, chunk: int = 0,
+          rows_cp: int | None = None) -> FFTPlan:
+    key = (precision, N, n_windows, T, prune_bins, chunk, rows_cp)
     p = _plans.get(key)
     if p is None:
         if len(_plans) >= 8:
             _plans.clear()
-        p = _plans[key] = FFTPlan(precision, N, n_windows, T, prune_bins, chunk)
+        p = _plans[key] = FFTPlan(precision, N, n_windows, T, prune_bins, chunk, rows_cp)
     return p
+
+
+ROWS_SPECTRUM_BYTES = 256 << 20     # compact spectrum of one rows-plan execution (rows_per_exec sizing)
+ROWS_MIN_OFFSETS = 8                # layout "auto": the rows plan from this many offsets per stream on
+
+
+def rows_per_exec(n_rows: int, n_br: int, T: int, n_bins: int, esz: int) -> int:
+    """Rows per rows-plan execution: a compact spectrum of about ROWS_SPECTRUM_BYTES, whole streams."""
+    per = max(n_br, (ROWS_SPECTRUM_BYTES // max(1, T * n_bins * esz)) // n_br * n_br)
+    return min(per, n_rows)
 
 
 def default_chunk(n_windows: int, n_br: int, N: int, esz: int) -> int:
@@ -160,7 +180,7 @@ CHUNK_BYTES = 64 << 20
 def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                             N: int | None = None, cp: int | None = None, *,
                                             return_peak: bool = False, pruned: bool = False,
-                                            chunk: int | None = None):
+                                            chunk: int | None = None, layout: str = "auto"):
     """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
     batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
     complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
@@ -172,7 +192,12 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     ``chunk``: windows per rocFFT execution (None or 0: one execution over the whole batch;
     ``default_chunk`` sizes one for the Infinity Cache); the spectrum scratch is [chunk][N].  Chunking
     keeps the spectrum round trip on-die but measured neutral on cfg5 (17.5 vs 17.7 ms): rocFFT's
-    own 4096-point kernel, not HBM, bounds the leg."""
+    own 4096-point kernel, not HBM, bounds the leg.
+    ``layout``: "offsets" - one rocFFT execution (+ gather) per offset, as above; "rows" - one execution
+    per group of rows covering every offset of them (windows one sample apart, always pruned:
+    ofs_zc_fft_plan_create_rows), 2 launches per row group instead of 2 per offset - the form for the
+    reference's own sliding shape (thousands of offsets per stream); "auto": "rows" from
+    ROWS_MIN_OFFSETS offsets per stream on when the template is prunable, else "offsets"."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -195,8 +220,31 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
             return (out, torch.empty((0,), dtype=torch.int64, device=dev),
                     torch.empty((0,), dtype=torch.float64, device=dev))
         return out
-    pruned = bool(pruned) and N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
+    prunable = N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
+    if layout not in ("auto", "offsets", "rows"):
+        raise ValueError("layout must be 'auto', 'offsets' or 'rows'")
+    if layout == "rows" and not prunable:
+        raise ValueError("layout='rows' needs a prunable template (N a power of two <= 4096, distinct bins)")
+    rows = layout == "rows" or (layout == "auto" and prunable and noff >= ROWS_MIN_OFFSETS)
+    pruned = (bool(pruned) or rows) and prunable
     nw = batch.B * batch.nb
+    out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
+    pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None
+    pv = torch.empty((batch.B,), dtype=torch.float64, device=dev) if return_peak else None
+    if rows:
+        esz = 8 if prec == _lib.FP32 else 16
+        rpe = int(chunk) if chunk else rows_per_exec(nw, batch.nb, batch.T, int(idx.size), esz)
+        if rpe % batch.nb:
+            raise ValueError("chunk (rows per execution) must be a multiple of the branch count")
+        plan = _plan(prec, N, nw, batch.T, int(idx.size), rpe, rows_cp=cp)
+        spec = torch.empty((plan.chunk, int(idx.size)), dtype=batch.data.dtype, device=dev)
+        work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
+        rc = _lib.lib().ofs_zc_freq_metric_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
+                                               batch.T, N, cp, int(idx.size), idx.ctypes.data, tb.ctypes.data,
+                                               float(template_energy), spec.data_ptr(), _lib.ptr(work),
+                                               out.data_ptr(), _lib.ptr(pk), _lib.ptr(pv), _lib.stream_ptr())
+        _lib.check(rc, "ofs_zc_freq_metric_fft")
+        return (out, pk, pv) if return_peak else out
     if chunk is None:
         chunk = 0                                       # one execution (chunking measured neutral)
     if chunk and chunk % batch.nb:
@@ -204,9 +252,6 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     plan = _plan(prec, N, nw, batch.T, int(idx.size) if pruned else 0, int(chunk))
     spec = torch.empty((plan.chunk, int(idx.size) if pruned else N), dtype=batch.data.dtype, device=dev)
     work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
-    out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
-    pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None
-    pv = torch.empty((batch.B,), dtype=torch.float64, device=dev) if return_peak else None
     rc = _lib.lib().ofs_zc_freq_metric_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
                                            batch.T, N, cp, int(idx.size), idx.ctypes.data, tb.ctypes.data,
                                            float(template_energy), spec.data_ptr(), _lib.ptr(work),

@@ -451,8 +451,8 @@ def test_zc_slide_templates_pair_and_fallback(tmpl, nb, variant):
 def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, variant):
     """FFT overlap-save matched filter (ofs_zc_correlate_fft) against the direct sums on the same
     samples, every combine mode: corr within 1e-11 of the row maximum, |corr| 1e-9 relative; for
-    8192-point blocks both the fused LDS-FFT kernel (default) and the rocFFT pipeline
-    (variant MC_FUSED=0)."""
+    8192-point blocks the persistent fused LDS-FFT kernel (default), the one-block-per-workgroup fused
+    kernel (variant MC_PERS=0) and the rocFFT pipeline (variant MC_FUSED=0)."""
     rng = np.random.default_rng(N + T + nb)
     B = 3
     x = rng_c(rng, B, nb, T) * 100
@@ -463,8 +463,9 @@ def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, variant):
         xd = torch.from_numpy(np.stack([np.round(x.real), np.round(x.imag)], -1).astype(np.int16)).cuda()
     else:
         xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
-    for fused in ("1", "0"):
-        variant("MC_FUSED", int(fused))
+    for fused in ("1", "1block", "0"):
+        variant("MC_FUSED", 0 if fused == "0" else 1)
+        variant("MC_PERS", 0 if fused == "1block" else None)
         for mode in (zc_v2.OFS_ZC_RAW, zc_v2.OFS_ZC_V2, zc_v2.OFS_ZC_COMBINED, zc_v2.OFS_ZC_SUM):
             cf, mf = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
             cd, md = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="direct")
@@ -473,6 +474,41 @@ def test_zc_fft_overlap_save_equals_direct(fmt, nb, N, T, variant):
             assert np.max(np.abs(cf - cd) / scale) < 1e-11, (mode, fused)
             np.testing.assert_allclose(mf, md, rtol=1e-9, atol=1e-11 * float(scale.max()))
     variant("MC_FUSED", None)
+    variant("MC_PERS", None)
+
+
+@pytest.mark.parametrize("fmt,nb,B,T", [("c128", 1, 300, 16384), ("c64", 1, 97, 20000), ("c128", 2, 150, 16384),
+                                        ("int16", 1, 700, 5000)])
+def test_zc_fft_persistent_kernel_many_blocks(fmt, nb, B, T, variant):
+    """The persistent matched-filter kernel (zc_fftcorr.hip mc_pers_kernel: one workgroup per CU walking
+    a run of 8192-point blocks, the next block's input prefetched during the current one) on batches
+    of more blocks than CUs, runs of unequal length and runs that cross stream boundaries: equal to
+    the one-block-per-workgroup kernel (variant MC_PERS=0) within 1e-12 of the row maximum, and to
+    the direct sums on sampled streams (1e-11 / |corr| 1e-9 relative), every output."""
+    rng = np.random.default_rng(B + T + nb)
+    ref = O.pss_symbol(2048)
+    x = rng_c(rng, B, nb, T) * 100
+    for b in range(0, B, 7):
+        s0 = int(rng.integers(0, T - 2048))
+        x[b, :, s0:s0 + 2048] += 100 * ref
+    if fmt == "int16":
+        xd = torch.from_numpy(np.stack([np.round(x.real), np.round(x.imag)], -1).astype(np.int16)).cuda()
+    else:
+        xd = torch.from_numpy(x.astype(np.complex64 if fmt == "c64" else np.complex128)).cuda()
+    for mode in (zc_v2.OFS_ZC_V2, zc_v2.OFS_ZC_RAW):
+        cp, mp = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
+        variant("MC_PERS", 0)
+        c1, m1 = zc_v2.correlate_batched(xd, ref, mode, want_corr=True, want_mag=True, method="fft")
+        variant("MC_PERS", None)
+        scale = c1.abs().amax(dim=-1, keepdim=True)
+        assert float(((cp - c1).abs() / scale).max()) < 1e-12, mode
+        np.testing.assert_allclose(mp.cpu().numpy(), m1.cpu().numpy(), rtol=1e-9, atol=1e-12 * float(scale.max()))
+        rows = torch.arange(0, B, max(1, B // 6), device=xd.device)
+        cd, md = zc_v2.correlate_batched(xd[rows], ref, mode, want_corr=True, want_mag=True, method="direct")
+        sc = cd.abs().amax(dim=-1, keepdim=True)
+        assert float(((cp[rows] - cd).abs() / sc).max()) < 1e-11, mode
+        np.testing.assert_allclose(mp[rows].cpu().numpy(), md.cpu().numpy(), rtol=1e-9,
+                                   atol=1e-11 * float(sc.max()))
 
 
 def test_zc_detect_four_branches_n2048_falls_back_to_direct():

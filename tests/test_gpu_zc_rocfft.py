@@ -137,8 +137,10 @@ def test_pruned_store_callback_equals_dense(prec, N, cp, T, nb):
     x = rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))
     xd = torch.from_numpy(x.astype(np.complex128 if prec == "c128" else np.complex64)).cuda()
     idx, t, e = zc_freq.make_pss_frequency_template()
-    a, pa, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=True)
-    b, pb, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=False)
+    a, pa, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=True,
+                                                               layout="offsets")
+    b, pb, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True, pruned=False,
+                                                               layout="offsets")
     tol = 1e-12 if prec == "c128" else 1e-5
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=tol, atol=tol * 1e-3)
     if prec == "c128":
@@ -164,9 +166,9 @@ def test_rocfft_chunked_equals_one_execution(prec, nb, chunk, pruned):
     idx, t, e = O.zc_template()
     xd = torch.from_numpy(x).cuda()
     m0, pk0, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
-                                                                 pruned=pruned, chunk=0)
+                                                                 pruned=pruned, chunk=0, layout="offsets")
     m1, pk1, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
-                                                                 pruned=pruned, chunk=chunk)
+                                                                 pruned=pruned, chunk=chunk, layout="offsets")
     a0, a1 = m0.cpu().numpy(), m1.cpu().numpy()
     tol = dict(rtol=1e-9, atol=1e-11)
     if prec == "c128":
@@ -186,3 +188,39 @@ def test_rocfft_chunk_must_split_branches():
     with pytest.raises(ValueError):
         zc_freq.compute_frequency_metric_rocfft_batched(torch.ones((4, 2, 80), dtype=torch.complex64).cuda(),
                                                         idx, t, e, N=64, cp=16, chunk=3)
+
+
+@pytest.mark.parametrize("prec,N,cp,T,nb,B,rpe", [("c128", 2048, 512, 4242, 2, 5, 0), ("c128", 2048, 512, 4242, 2, 5, 4),
+                                                  ("c64", 2048, 512, 4242, 2, 64, 0), ("c128", 256, 32, 700, 3, 7, 6),
+                                                  ("c64", 128, 0, 1000, 1, 33, 5)])
+def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe):
+    """The rows plan (ofs_zc_fft_plan_create_rows: every offset of a row group in ONE rocFFT execution,
+    windows one sample apart, the callback dropping the windows that straddle two rows) gives the
+    per-offset plan's metric and argmax on the reference's own sliding shape (T = 4242, 2 branches,
+    N = 2048, cp = 512: 1683 offsets), with row groups that leave a tail; fp64 also vs the oracle,
+    complex64 within error model 2 on every window."""
+    rng = np.random.default_rng(N + T + B)
+    x = rng_c(rng, B, nb, T)
+    sym = O.pss_symbol(N)
+    for b in range(0, B, 3):
+        s0 = int(rng.integers(0, T - N - cp))
+        x[b, :, s0 + cp:s0 + cp + N] += 3 * sym
+    x = x.astype(np.complex128 if prec == "c128" else np.complex64)
+    idx, t, e = O.zc_template()
+    xd = torch.from_numpy(x).cuda()
+    r, pr, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                               layout="rows", chunk=rpe)
+    o, po, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                               layout="offsets", pruned=True)
+    a, b_ = r.cpu().numpy(), o.cpu().numpy()
+    assert a.shape == (B, T - N - cp + 1)
+    if prec == "c128":
+        np.testing.assert_allclose(a, b_, rtol=1e-12, atol=1e-14)
+        assert torch.equal(pr, po)
+        for k in (0, B - 1):
+            np.testing.assert_allclose(a[k], O.zc_freq_metric(x[k], N, cp, idx, t, e), rtol=1e-9, atol=1e-11)
+    else:
+        st = oracle_c.zc_freq_check(x, N, cp, idx, t, e, a, EM.rocfft_eps(N), 6.0)
+        print(f"rows c64 N={N}: max |dm|/bound {st[:, 1].max():.3g}")
+        assert st[:, 1].max() <= 1.0
+        np.testing.assert_allclose(a, b_, rtol=1e-5, atol=1e-8)

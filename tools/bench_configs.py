@@ -528,7 +528,10 @@ def zc_mf(dev, st, steps, warmup, method="fft"):
         # once per block (M samples incl. the N-1 overlap), corr + |corr| written once; no scratch
         traffic = B * nblk * M * 16 + B * nout * 24
         model = "x read once per block (M = 8192 incl. the N-1 overlap) + corr 16 B + |corr| 8 B out"
-        kern = "mc_fused_kernel<C128, fused extract>: load + DIF FFT + xH/M + DIT inverse + normalise in LDS"
+        kern = ("mc_fused_kernel<C128, fused extract>: load + DIF FFT + xH/M + DIT inverse + normalise in LDS"
+                if _lib.get_variant("MC_PERS") == 0 else
+                "mc_pers_kernel<C128, fused extract>: persistent, one 512-thread workgroup per CU; next block "
+                "prefetched; DIF FFT + xH/M + DIT inverse + normalise in LDS")
     else:
         spec = B * nblk * M * 16
         traffic = (B * T * 16 + spec) + 2 * spec + 2 * spec + 2 * spec + (B * nout * 16 + B * T * 16 + B * nout * 24)
