@@ -464,12 +464,40 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
 //                spans   16..1   LDS pass, elements 16t + i, lane pairs (span 16 across the pair by DPP)
 //   conj(X * H / M) in bit-reversed order (Hbr, as mc_fused_kernel)
 //   inverse DIT  spans 1..16 (same pass), 32..256 (LDS pass), 512..4096 (registers)
-// 4 LDS passes instead of 5, each stage's twiddle one product with a per-thread base (bases from a
-// table built once per launch).  gfx9 counts loads and stores on one vmcnt and they complete out of
+// 4 LDS passes instead of 5, two of them wave-local (no workgroup barrier), each stage's twiddle one
+// product with a per-thread base (bases from a table built once per launch).  gfx9 counts loads and stores on one vmcnt and they complete out of
 // order, so waiting for any load waits for every store in flight: the Hbr slice is loaded right after
 // the previous block's stores (waited for in the middle pass, by when those stores have drained), and the
 // next block's input is taken into registers BEFORE this block's stores are issued.
 constexpr int MP_T = 512;
+#ifndef OFS_MP_NTST
+#define OFS_MP_NTST 1               // non-temporal output stores (measured 3-6 % faster, profiles/r05j_*)
+#endif
+#ifndef OFS_MP_CLAMPLOAD
+#define OFS_MP_CLAMPLOAD 0
+#endif
+#ifndef OFS_MP_AB
+#define OFS_MP_AB 0                 // diagnostic A/B builds only (wrong results): 1 no stores, 2 no sqrt/div,
+#endif                              // 4 no energy prefix (the extract's LDS phase and its barriers), 8 no H loads
+#ifndef OFS_MP_TIMING
+#define OFS_MP_TIMING 0             // diagnostic builds: per-phase cycles of mc_pers_kernel (ofs_mp_prof)
+#endif
+#if OFS_MP_TIMING
+__device__ unsigned long long mp_prof[8];
+#endif
+// LDS hand-over between the lanes of ONE wave: its LDS operations complete in order
+#ifndef OFS_MP_WAVESYNC
+#define OFS_MP_WAVESYNC 1           // tuning builds: 0 = workgroup barriers there as well
+#endif
+__device__ __forceinline__ void mp_wave_sync() {
+#if OFS_MP_WAVESYNC
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+    mf_sync();
+#endif
+}
 constexpr int MP_LDS = (MF_M + 512 + 32) * 16 + 8 * 8;   // block, w_8192^t (t < 512), w_512^k (k < 32), wave sums
 // slot of block element e: low four bits XOR bits 4-7 (conflict-free for t + 512m, 512g + 32i + k, 16t + i)
 __device__ __forceinline__ int mp_at(int e) { return e ^ ((e >> 4) & 15); }
@@ -560,15 +588,37 @@ __device__ __forceinline__ void mp_dit16(double2 (&v)[16], double2 b) {
     }
 }
 
+// 1/sqrt(x) for normal x > 0: v_rsq_f64 and two Newton steps y(1.5 - x y^2/2)
+__device__ __forceinline__ double mp_rsqrt(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double h = x * y;
+        y = fma(0.5 * y, fma(-h, y, 1.0), y);
+    }
+    return y;
+}
+// sqrt(x), x >= 0: x rsqrt(x) for normal x, the library sqrt below 2^-1000 (0 and denormals)
+__device__ __forceinline__ double mp_sqrt(double x) {
+    if (x < 0x1p-1000) return sqrt(x);
+    return x * mp_rsqrt(x);
+}
+
+// a block's samples t + 512m (zero outside the stream)
 template <int FMT>
-__device__ __forceinline__ void mp_load(const McArgs& a, int64_t blk, int t, double2 (&d)[16]) {
-    const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+__device__ __forceinline__ void mp_load(const McArgs& a, int64_t row, int64_t q, int t, double2 (&d)[16]) {
     const int64_t g0 = q * a.S - (a.N - 1) + t;
     const int64_t base = row * a.T;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const int64_t g = g0 + MP_T * m;
+#if OFS_MP_CLAMPLOAD                // tuning builds: every lane loads a clamped in-stream index, then selects
+        const bool in = g >= 0 && g < a.T;
+        const double2 w = ldx<FMT>(a.x, base + (in ? g : 0));
+        d[m] = in ? w : make_double2(0.0, 0.0);
+#else
         d[m] = (g >= 0 && g < a.T) ? ldx<FMT>(a.x, base + g) : make_double2(0.0, 0.0);
+#endif
     }
 }
 
@@ -590,16 +640,31 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
     }
     const int64_t G = gridDim.x, wg = blockIdx.x;
     const int64_t b0 = wg * total / G, b1 = (wg + 1) * total / G;   // this workgroup's run of blocks
+    const double rn_inv = 1.0 / a.ref_norm;
     if (b0 >= b1) return;                                           // (whole workgroup)
     double2 v[16];
     double en[FUSE_X ? 16 : 1];                                     // |u|^2 of this block's samples t + 512m
-    mp_load<FMT>(a, b0, t0, v);
+    int64_t row = b0 / a.nblk, q = b0 - (b0 / a.nblk) * a.nblk;   // block b0 = row * nblk + q (then stepped)
+    mp_load<FMT>(a, row, q, t0, v);
     if constexpr (FUSE_X) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) en[m] = fma(v[m].x, v[m].x, v[m].y * v[m].y);
     }
+#if OFS_MP_TIMING
+    unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tl = __builtin_readcyclecounter();
+#define MP_T_MARK(i) do { const unsigned long long tn = __builtin_readcyclecounter(); tacc[i] += tn - tl; tl = tn; } while (0)
+#else
+#define MP_T_MARK(i) do { } while (0)
+#endif
+#if OFS_MP_AB & 1
+    const bool st_ok = a.T < 0;                                     // diagnostic: no stores
+#else
+    constexpr bool st_ok = true;
+#endif
     for (int64_t blk = b0; blk < b1; ++blk) {
-        const int64_t row = blk / a.nblk, q = blk - row * a.nblk;
+        if (blk > b0 && ++q == a.nblk) { q = 0; ++row; }          // (no 64-bit division per block)
+        const int64_t nq = q + 1 == a.nblk ? 0 : q + 1, nrow = nq == 0 ? row + 1 : row;   // the next block
         // the thread index re-materialised per block (opaque to the optimiser): the per-thread LDS
         // addresses, twiddle bases and the H slice are loop-invariant, and hoisting them out of the block
         // loop would pin ~100 VGPRs for the whole launch
@@ -608,10 +673,12 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
         const int g2 = t >> 5, k2 = t & 31;                          // LDS pass position: 512 g2 + 32 i + k2
         // ---- forward: spans 4096..512 in registers ----
         mp_dif16<false>(v, tb[t]);
+        MP_T_MARK(0);
         mf_sync();                                                  // previous block's LDS readers done
 #pragma unroll
         for (int m = 0; m < 16; ++m) fb[mp_at(t + MP_T * m)] = v[m];
         mf_sync();
+        MP_T_MARK(1);
         // ---- spans 256..32 ----
         {
             const int p = 512 * g2 + k2;
@@ -621,7 +688,11 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
 #pragma unroll
             for (int i = 0; i < 16; ++i) fb[mp_at(p + 32 * i)] = v[i];
         }
-        mf_sync();
+        // spans 256..1 and back stay inside the 512 elements of group g2 = t / 32, which the half-wave t / 32
+        // owns in this pass and the next: a wave-local hand-over, no workgroup barrier (the waves drift apart,
+        // so one wave's LDS traffic overlaps another's arithmetic)
+        mp_wave_sync();
+        MP_T_MARK(2);
         // ---- spans 16..1, conj(X H / M), spans 1..16: lane pair (t, t^1) holds elements 32(t/2) .. +31 ----
         {
             const bool hi = (t & 1) != 0;
@@ -629,7 +700,7 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             // (one vmcnt), which have had the first two passes to drain
             double2 hb[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) hb[i] = Hbr[16 * t + i];
+            for (int i = 0; i < 16; ++i) hb[i] = (OFS_MP_AB & 8) ? make_double2(1.0, 0.0) : Hbr[16 * t + i];
 #pragma unroll
             for (int i = 0; i < 16; ++i) v[i] = fb[mp_at(16 * t + i)];
 #pragma unroll
@@ -654,12 +725,13 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
 #pragma unroll
             for (int i = 0; i < 16; ++i) fb[mp_at(16 * t + i)] = v[i];
         }
-        mf_sync();
+        mp_wave_sync();
+        MP_T_MARK(3);
         // the next block's input: in flight through the second half of this block
         const bool more = blk + 1 < b1;
         double2 nx[16];
         if (more) {
-            mp_load<FMT>(a, blk + 1, t, nx);
+            mp_load<FMT>(a, nrow, nq, t, nx);
         } else {
 #pragma unroll
             for (int m = 0; m < 16; ++m) nx[m] = make_double2(0.0, 0.0);
@@ -674,9 +746,11 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             for (int i = 0; i < 16; ++i) fb[mp_at(p + 32 * i)] = v[i];
         }
         mf_sync();
+        MP_T_MARK(4);
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = fb[mp_at(t + MP_T * m)];
         mp_dit16<false>(v, tb[t]);                                  // spans 512..4096: natural order out
+        MP_T_MARK(5);
         const int64_t n0 = q * a.S;
         const int ns = (int)min((int64_t)a.S, a.nout - n0);
         if constexpr (!FUSE_X) {
@@ -694,8 +768,9 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
         // ---- fused extract (one branch): window energies from an fp64 prefix of |u|^2 in the block LDS ----
         // P[j] = sum_{i<j} |u_i|^2 in place of |u_j|^2 (each thread rewrites only the 16 slots it read, so
         // no neighbour's input is overwritten), P[M] at slot mp_pq(M)
-        mf_sync();                                                  // every thread has read its block slots
         double* P = reinterpret_cast<double*>(fb);
+#if !(OFS_MP_AB & 4)
+        mf_sync();                                                  // every thread has read its block slots
 #pragma unroll
         for (int m = 0; m < 16; ++m) P[mp_pq(t + MP_T * m)] = en[m];
         mf_sync();
@@ -715,6 +790,7 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             run += e;
         }
         if (t == MP_T - 1) P[mp_pq(MF_M)] = run;
+#endif
         // next block's input taken into registers (and its energies) before any store of this block issues
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
@@ -724,6 +800,7 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             en[m] = fma(v[m].x, v[m].x, v[m].y * v[m].y);
         }
         mf_sync();
+        MP_T_MARK(6);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
@@ -732,19 +809,36 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             const double2 c = make_double2(nx[m].x, -nx[m].y);
             const int64_t oi = row * a.nout + n0 + s;               // one branch: row = stream
             if (a.mode == OFS_ZC_RAW || a.mode == OFS_ZC_SUM) {
-                if (a.out) a.out[oi] = c;
-                if (a.mag) a.mag[oi] = sqrt(fma(c.x, c.x, c.y * c.y));
+                if (a.out && st_ok) a.out[oi] = c;
+                if (a.mag && st_ok) a.mag[oi] = mp_sqrt(fma(c.x, c.x, c.y * c.y));
                 continue;
             }
+#if OFS_MP_AB & 4
+            const double e = 1.0 + en[m];
+#else
             const double e = P[mp_pq(o + 1)] - P[mp_pq(o + 1 - a.N)];   // sum |x|^2 over the N-sample window
+#endif
             const double ewc = a.mode == OFS_ZC_V2 ? (e > 1e-12 ? e : 1e-12)                 // zc_v2.py:268
                                                    : (e > 0.0 ? e : 0.0) + 1e-12;            // zc.py:113-126
-            const double inv = 1.0 / (a.ref_norm * sqrt(ewc));
+            // 1 / (|ref| sqrt(e)) = rsqrt(e) / |ref| and |r| = s rsqrt(s), s = |r|^2: hardware rsqrt refined by
+            // two Newton steps (an ulp or two from the reference's division and hypot, zc_v2.py:268-271)
+            const double inv = mp_rsqrt(ewc) * rn_inv;
             const double2 r = make_double2(c.x * inv, c.y * inv);
-            if (a.out) a.out[oi] = r;
-            if (a.mag) a.mag[oi] = sqrt(fma(r.x, r.x, r.y * r.y));
+#if OFS_MP_NTST                     // tuning builds: non-temporal output stores
+            if (a.out && st_ok) { __builtin_nontemporal_store(r.x, &a.out[oi].x); __builtin_nontemporal_store(r.y, &a.out[oi].y); }
+            if (a.mag && st_ok) __builtin_nontemporal_store(mp_sqrt(fma(r.x, r.x, r.y * r.y)), &a.mag[oi]);
+#else
+            if (a.out && st_ok) a.out[oi] = r;
+            if (a.mag && st_ok) a.mag[oi] = mp_sqrt(fma(r.x, r.x, r.y * r.y));
+#endif
         }
+        MP_T_MARK(7);
     }
+#if OFS_MP_TIMING
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&mp_prof[i], tacc[i]);
+#endif
+#undef MP_T_MARK
 }
 
 // Hbr[i] = H[bitrev(i)] / M, for the fused path; then the kernel's two 64-entry twiddle tables
@@ -1079,4 +1173,12 @@ int32_t ofs_zc_correlate_fft(void* plan, int32_t in_fmt, const void* x, int64_t 
     return hipGetLastError() == hipSuccess ? OFS_OK : OFS_EHIP;
 }
 
+#if OFS_MP_TIMING
+// per-phase cycle totals of mc_pers_kernel (summed over waves) since the last call (diagnostic builds)
+int32_t ofs_mp_prof(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mp_prof), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(mp_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"

@@ -16,6 +16,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libofdmsync.so")       # the in-tree build (no environment override)
 TUNING_BUILD = None          # set by use_tuning_library(): name of the tools/variants.py build in use
+_TUNING_PATH = None
 
 # input formats / precisions / status (include/ofdmsync.h)
 C64, C128, CI16, CP12 = 0, 1, 2, 3
@@ -177,16 +178,18 @@ def use_tuning_library(path: str) -> str:
     """Measurement tools only: load a tuning build of tools/variants.py (the sources compiled with
     extra -D flags; its baked hash reads ``variant-<name>``) instead of the in-tree library.  Must
     run before the library is first used; any other library is refused.  Returns the build name."""
-    global _lib, TUNING_BUILD
+    global _lib, TUNING_BUILD, _TUNING_PATH
+    path = os.path.abspath(path)
+    if _lib is not None and _TUNING_PATH == path:
+        return TUNING_BUILD                                  # the same build again: already in use
     if _lib is not None:
         raise RuntimeError("use_tuning_library() must run before the library is first loaded")
-    path = os.path.abspath(path)
     l = ctypes.CDLL(path)
     built = _baked_hash(l)
     if not built.startswith("variant-"):
         raise ImportError(f"{path} is not a tools/variants.py tuning build (hash {built})")
     _declare(l)
-    _lib, TUNING_BUILD = l, built[len("variant-"):]
+    _lib, TUNING_BUILD, _TUNING_PATH = l, built[len("variant-"):], path
     return TUNING_BUILD
 
 

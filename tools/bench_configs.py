@@ -595,6 +595,35 @@ def zc_freq_refshape(dev, st, steps, warmup, B=4096):
                   B * noff * 62 * (12 * nb + 10), "fp64")
 
 
+def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows"):
+    """The north-star rocFFT formulation of zc_freq.compute_frequency_metric (zc_freq.py:62-99: one FFT per
+    window) at the reference's own sliding shape (T = 4242, 2 branches, N = 2048, cp = 512: 1683 offsets
+    per stream), complex64, B streams.  layout "rows": ofs_zc_fft_plan_create_rows - every offset of a row
+    group in one rocFFT execution (windows one sample apart, pruned by the store callback; T windows per
+    row are transformed for n_off used); "offsets": one execution + gather per offset (2 x 1683 launches
+    per row group).  Bound: the FFT flops (5 N log2 N per transformed window) against the fp32 vector
+    peak - the sliding DFT (zc_freq_refshape) does O(62) work per offset instead of O(N log N)."""
+    T, N, cp, nb = 4242, 2048, 512, 2
+    g = torch.Generator(device=dev).manual_seed(8)
+    x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    ms = timed(lambda: zc_freq.compute_frequency_metric_rocfft_batched(x, N=N, cp=cp, layout=layout,
+                                                                       pruned=True), steps, warmup, st)
+    noff = T - (N + cp) + 1
+    windows = B * nb * (T if layout == "rows" else noff)
+    fft_flops = windows * 5 * N * 11
+    r = dict(config="zc_freq_refshape_rocfft" + ("" if layout == "rows" else "_offsets"),
+             workload=f"zc_freq N={N} cp={cp}, {B} x {nb} x {T} c64 -> f32 via rocFFT ({layout} layout)",
+             kernel=("rocFFT fp32 C2C over every offset of a row group per execution (in_dist 1, pruning store "
+                     "callback) + zc_gather_rows_kernel" if layout == "rows" else
+                     "per offset: rocFFT fp32 C2C (pruned) + zc_gather_kernel"),
+             samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4, transformed_windows=windows,
+             launches_per_call=(2 * -(-B * nb // zc_freq.rows_per_exec(B * nb, nb, T, 62, 8)) if layout == "rows"
+                                else 2 * noff), bytes_per_sample="8 in + 4 out per offset")
+    r.update(fft_flops=fft_flops, fft_tflops=round(fft_flops / (ms / 1e3) / 1e12, 2),
+             fft_flop_frac_fp32=round(fft_flops / (ms / 1e3) / 157.3e12, 4))
+    return r
+
+
 def zc_detect(dev, st, steps, warmup, state=False, seq=False):
     """zc_v2 CFAR + gate (zc_v2.py:300-446) on |corr| rows: B = 4096 x 16384 f64.  Default kernel:
     zc_cfar_kernel (lane-per-stream exact recursion + closed-form gate, zc_cfar.hip); seq=True times
@@ -620,6 +649,8 @@ def zc_detect(dev, st, steps, warmup, state=False, seq=False):
 
 CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "park_fp32": park, "park_fp64": lambda *a, **k: park(*a, prec="fp64", **k), "zc_mf": zc_mf,
            "zc_freq_fp64": zc_freq_fp64, "zc_freq_refshape": zc_freq_refshape, "zc_detect": zc_detect,
+           "zc_freq_refshape_rocfft": zc_freq_refshape_rocfft,
+           "zc_freq_refshape_rocfft_offsets": lambda *a, **k: zc_freq_refshape_rocfft(*a, layout="offsets", **k),
            "zc_detect_state": lambda *a, **k: zc_detect(*a, state=True, **k),
            "zc_detect_seq": lambda *a, **k: zc_detect(*a, seq=True, **k),
            "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
