@@ -47,8 +47,10 @@ def timed(step, steps, warmup, stream):
     """HIP events over `steps` calls after `warmup` untimed calls, continued until WARM_MS of wall
     time have passed: sub-millisecond kernels reach steady clocks only after some tens of ms of load
     (zc_freq_refshape 0.62 ms after 5 calls vs 0.553 ms steady, tools/lib_ab.py rounds)."""
+    step()                          # first call: plan creation / lazy set-up outside the warm-up clock
+    torch.cuda.synchronize()
     t_w = time.perf_counter()
-    n = 0
+    n = 1
     while n < warmup or (time.perf_counter() - t_w) * 1e3 < WARM_MS:
         step()
         n += 1
