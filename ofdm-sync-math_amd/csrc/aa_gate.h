@@ -28,6 +28,12 @@ namespace ofs {
 #ifndef OFS_GATE_FASTFLAGS
 #define OFS_GATE_FASTFLAGS 1
 #endif
+#ifndef OFS_GATE_DIAG
+#define OFS_GATE_DIAG 0
+#endif
+#ifndef OFS_GATE_NOACC
+#define OFS_GATE_NOACC 0
+#endif
 #ifndef OFS_GATE_DEFER
 #define OFS_GATE_DEFER 1
 #endif
@@ -84,9 +90,19 @@ struct AaRowGate {
     // sync_aa row (all positions >= L): above = m >= threshold; m = metric, pm = |P|², pr/pi = P
     __device__ __forceinline__ void row(int lane, int k, int nb, int T, const V (&m)[E], const V (&pm)[E],
                                         const V (&pr)[E], const V (&pi)[E]) {
+#if OFS_GATE_DIAG == 1              // diagnostic builds only (wrong events): no row work at all
+        return;
+#endif
         bool ab[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) ab[e] = (nb + e < T) && (double)m[e] >= thr;
+#if OFS_GATE_DIAG == 2              // diagnostic builds only: the above ballots, nothing else
+        uint64_t any = 0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) any |= __ballot(ab[e]);
+        if (any) carry_last = RL * k;
+        return;
+#endif
         row_flags(lane, k, nb, T, ab, pm, pr, pi, m);
     }
 
@@ -101,6 +117,9 @@ struct AaRowGate {
     }
     __device__ __forceinline__ void accumulate(int lane, int k, int nb, int T, int lo, int hi, const V (&pm)[E],
                                                const V (&pr)[E], const V (&pi)[E], const V (&m)[E]) {
+#if OFS_GATE_NOACC                  // diagnostic builds only (wrong peaks): no per-lane peak tracking
+        return;
+#endif
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int key = E * lane + e;
