@@ -117,7 +117,7 @@ struct AaRowGate {
     }
     __device__ __forceinline__ void accumulate(int lane, int k, int nb, int T, int lo, int hi, const V (&pm)[E],
                                                const V (&pr)[E], const V (&pi)[E], const V (&m)[E]) {
-#if OFS_GATE_NOACC                  // diagnostic builds only (wrong peaks): no per-lane peak tracking
+#if OFS_GATE_NOACC == 1             // diagnostic builds only (wrong peaks): no per-lane peak tracking
         return;
 #endif
 #pragma unroll
@@ -125,7 +125,11 @@ struct AaRowGate {
             const int key = E * lane + e;
             const bool in = nb + e < T && key >= lo && key <= hi;
             const bool better = RTL ? (pm[e] >= lv) : (pm[e] > lv);
+#if OFS_GATE_NOACC == 2             // diagnostic builds only (wrong payload): value + index tracked
+            if (in && better) { lv = pm[e]; lk = RL * k + key; }
+#else
             if (in && better) { lv = pm[e]; lk = RL * k + key; lpr = pr[e]; lpi = pi[e]; lm = m[e]; }
+#endif
         }
     }
     // wave reduction of the lanes' running bests into the event's peak (kept if it beats the

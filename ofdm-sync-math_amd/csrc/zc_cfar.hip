@@ -31,15 +31,16 @@ using namespace ofs;
 
 namespace {
 
-// streams per workgroup (walker lanes) and helper waves: LDS-DMA path 16 streams, 7 helpers (one
-// workgroup of 8 waves per CU; static LDS (4 + 3 + 2) x 16 x 130 doubles = 149,760 B = 146.25 KiB of
+// streams per workgroup (walker lanes) and helper waves: LDS-DMA path 16 streams, 11 helpers (one
+// workgroup of 12 waves per CU, 154 VGPRs = 3 waves/SIMD; round 5, paired builds on zc_detect: 7 / 8 /
+// 11 / 15 helpers 0.306 / 0.289 / 0.286 / 0.492 ms, profiles/r05p_zc_cfar_helpers_ab.txt; static LDS (4 + 3 + 2) x 16 x 130 doubles = 149,760 B = 146.25 KiB of
 // gfx950's 160 KiB, asserted in the kernel); register path 8 streams, 3 helpers ((3 + 2 + 2) x 8 x
 // 130 doubles = 57 KiB; its staging registers scale with the stream count)
 #ifndef OFS_ZC_S
 #define OFS_ZC_S 16
 #endif
 #ifndef OFS_ZC_H
-#define OFS_ZC_H 7
+#define OFS_ZC_H 11
 #endif
 #ifndef OFS_ZC_S_REG
 #define OFS_ZC_S_REG 8
