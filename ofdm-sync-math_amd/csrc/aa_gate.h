@@ -28,6 +28,12 @@ namespace ofs {
 #ifndef OFS_GATE_FASTFLAGS
 #define OFS_GATE_FASTFLAGS 1
 #endif
+#ifndef OFS_GATE_NOINLINE_EMIT
+#define OFS_GATE_NOINLINE_EMIT 0
+#endif
+#ifndef OFS_GATE_FFONLY
+#define OFS_GATE_FFONLY 0
+#endif
 #ifndef OFS_GATE_DIAG
 #define OFS_GATE_DIAG 0
 #endif
@@ -63,7 +69,11 @@ struct AaRowGate {
     // the record is wave-uniform: lanes 0..3 store the four int64 fields and lanes 4..7 the four
     // f64 fields, one store instruction per 32-byte record half (a lane-0 loop of 8-byte stores
     // cost ~450 B of write traffic per event, measured with WRITE_SIZE)
+#if OFS_GATE_NOINLINE_EMIT
+    __device__ __attribute__((noinline)) void emit(int lane, int gate_end) {
+#else
     __device__ __forceinline__ void emit(int lane, int gate_end) {
+#endif
         if (evi && n_ev < max_ev && lane < 8) {
             int64_t* ei = evi + (int64_t)n_ev * 4;
             if constexpr (RTL) {
@@ -134,7 +144,11 @@ struct AaRowGate {
     }
     // wave reduction of the lanes' running bests into the event's peak (kept if it beats the
     // peak so far under the machine's tie rule), then the lanes restart
+#if OFS_GATE_NOINLINE_EMIT
+    __device__ __attribute__((noinline)) void merge() {
+#else
     __device__ __forceinline__ void merge() {
+#endif
         const V vmax = wave_max(lv);
         const int kk = RTL ? wave_max_i(lv == vmax ? lk : -1) : wave_min(lv == vmax ? lk : ABS_NOKEY);
         const bool found = RTL ? (kk >= 0) : (kk != ABS_NOKEY);
@@ -163,7 +177,7 @@ struct AaRowGate {
     __device__ __forceinline__ void row_flags(int lane, int k, int nb, int T, const bool (&ab)[E],
                                               const V (&pm)[E], const V (&pr)[E], const V (&pi)[E],
                                               const V (&m)[E]) {
-        if (FF && OFS_GATE_FASTFLAGS && Hp >= RL) {
+        if (FF && OFS_GATE_FASTFLAGS && (OFS_GATE_FFONLY || Hp >= RL)) {
             // hysteresis at least one row: only the row's FIRST above sample can open a gate and
             // only carry_last + Hp can close one (before that first sample), so the machine runs
             // on the above ballots alone, in scalar registers - no prefix scan
@@ -197,6 +211,9 @@ struct AaRowGate {
             if (gate_open) seg(lane, k, nb, T, seg_lo, RL - 1, pm, pr, pi, m);
             return;
         }
+#if OFS_GATE_FFONLY                 // diagnostic builds only (H >= one row assumed): no scan path
+        return;
+#endif
         int lane_last = -1;
 #pragma unroll
         for (int e = 0; e < E; ++e)

@@ -22,15 +22,18 @@ pytestmark = pytest.mark.gpu
 B, T, L = 8192, 1024, 512
 
 
-@pytest.fixture(scope="module")
-def run():
+@pytest.fixture(scope="module", params=["default", "scan32", "scan64"])
+def run(request):
+    """The storing kernel with its default row scans, and each scan precision forced (variant FAST_SCAN)."""
     import oracle_c
-    from ofdm_sync_amd import sync_aa, synth
+    from ofdm_sync_amd import _lib, sync_aa, synth
     dev = torch.device("cuda", 0)
     det = sync_aa.AABatchDetector(B, T, 1, L, outputs=("P", "R", "M"), max_events=8, device=dev)
     det.x.copy_(synth.make_aa_batch(B, T, L, seed=4242, device=dev))
-    res = det.run()
-    torch.cuda.synchronize()
+    forced = {"default": None, "scan32": 32, "scan64": 64}[request.param]
+    with _lib.variants(FAST_SCAN=forced):
+        res = det.run()
+        torch.cuda.synchronize()
     xh = det.x.cpu().numpy()
     o = oracle_c.aa_detect(xh, L, max_events=8, nthreads=min(16, os.cpu_count() or 1))
     g = dict(P=res.P.cpu().numpy(), R=res.R.cpu().numpy(), M=res.M.cpu().numpy().astype(np.float64),

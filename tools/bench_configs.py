@@ -406,6 +406,27 @@ def cfg3_detect(dev, st, steps, warmup):
                 bytes_per_sample="8 in + 4 B/stream + 64 B/event", events_per_stream=round(stored / B, 3))
 
 
+def cfg3(dev, st, steps, warmup):
+    """cfg3 = bench.py's headline launch (sync_aa storing kernel: P, R, M + events, 65536 x 1024 c64,
+    L = 512) on plain caching-allocator buffers, for variant A/Bs (tools/variant_ab.py); bench.py's
+    own line (AABatchDetector, contiguous placement) is the number of record."""
+    B, T, L, E = 65536, 1024, 512, 4
+    x = synth.make_aa_batch(B, T, L, seed=2026, device=dev)
+    P = torch.empty((B, T), dtype=torch.complex64, device=dev)
+    R = torch.empty((B, T), dtype=torch.float32, device=dev)
+    M = torch.empty_like(R)
+    n_ev = torch.zeros(B, dtype=torch.int32, device=dev)
+    ev_i = torch.empty((B, E, 4), dtype=torch.int64, device=dev)
+    ev_r = torch.empty((B, E, 4), dtype=torch.float64, device=dev)
+    L_ = _lib.lib()
+    args = (_lib.C64, x.data_ptr(), B, 1, T, L, _lib.FP32, P.data_ptr(), R.data_ptr(), M.data_ptr(), None, 1,
+            0.15, 128, 15.36e6, E, n_ev.data_ptr(), ev_i.data_ptr(), ev_r.data_ptr(), st.cuda_stream)
+    ms = timed(lambda: chk(L_.ofs_aa_detect(*args), "aa"), steps, warmup, st)
+    return dict(config="cfg3", workload=f"sync_aa S&C fp32 + events, L={L}, {B} x {T} c64",
+                kernel="aa_fast_kernel<2,4,1> (P, R, M + events)", samples=B * T, ms=ms, alg_bytes=B * T * 24,
+                bytes_per_sample="8 in + 16 out")
+
+
 def cfg3_pcie(dev, st, steps, warmup):
     """cfg3 with the batch handed over in host memory (the numpy drop-in's situation): pinned host
     x -> HBM, the headline kernel, P/R/M back to pinned host, all on one stream.  The PCIe-inclusive
@@ -659,7 +680,7 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
            "cfg5_rocfft_chunked": lambda *a, **k: cfg5_rocfft(*a, pruned=False, chunked=True, **k),
            "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
-"cfg2a": cfg2a, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
+"cfg2a": cfg2a, "cfg3": cfg3, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
 
 
 def _selftest_config(name):
