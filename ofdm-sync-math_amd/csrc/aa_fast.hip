@@ -91,6 +91,13 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 #ifndef OFS_FAST_FF
 #define OFS_FAST_FF 0
 #endif
+// tuning builds: 1 = gate machine after the row loop - each row's (M, |P|^2, P) of the gated rows goes to
+// a wave-private LDS slice and the gate runs over them once every row's stores have issued.  Measured
+// (paired, profiles/r05_headline_gate_breakdown.txt): neutral on the headline (0.2937-0.3053 vs
+// 0.2924-0.3056 ms), 5 % slower detect-only (0.107 vs 0.102 ms); default 0 = per row
+#ifndef OFS_FAST_GATE_LATE
+#define OFS_FAST_GATE_LATE 0
+#endif
 // DO: detect-only instantiation (P/R/M/valid not stored, events only: SURVEY §8d); S32: fp32
 // row scans (ofs_common.h row_scan; the detect-only default, issue-bound there)
 template <int E, int MR, int NA, bool DO, bool S32>
@@ -169,6 +176,10 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
     AaRowGate<E, float, false, (bool)(DO || OFS_FAST_FF)> gate;   // event state (wave-uniform)
+#if OFS_FAST_GATE_LATE
+    constexpr int GR = RW - MR > 0 ? RW - MR : 1;             // gated rows (k >= MR)
+    __shared__ float4 gl[FAST_WG / 64][GR][E][64];            // (M, |P|^2, Re P, Im P) per sample
+#endif
     if (a.detect)
         gate.init(a.hyst, L, a.thr, a.fs, a.max_ev, a.ev_i + b * (int64_t)a.max_ev * 4,
                   a.ev_r + b * (int64_t)a.max_ev * 4);
@@ -263,13 +274,37 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 
             // ---- events: closed-form gate machine, streamed per row (aa_gate.h) ----
             if (a.detect && k >= MR) {
+#if OFS_FAST_GATE_LATE
+#pragma unroll
+                for (int e = 0; e < E; ++e) gl[w][k >= MR ? k - MR : 0][e][lane] = make_float4(mf[e], pmf[e], pf[e][0], pf[e][1]);
+#else
                 float pr[E], pi[E];
 #pragma unroll
                 for (int e = 0; e < E; ++e) { pr[e] = pf[e][0]; pi[e] = pf[e][1]; }
                 gate.row(lane, k, nb, T, mf, pmf, pr, pi);
+#endif
             }
         }
     }
+#if OFS_FAST_GATE_LATE
+    if (a.detect) {
+        // this wave's own LDS slice, written lane-wise above: a wave-local hand-over
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+        for (int k = MR; k < RW; ++k) {
+            if (RL * k >= T) break;
+            float m[E], pm[E], pr[E], pi[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const float4 v = gl[w][k - MR][e][lane];
+                m[e] = v.x; pm[e] = v.y; pr[e] = v.z; pi[e] = v.w;
+            }
+            gate.row(lane, k, RL * k + E * lane, T, m, pm, pr, pi);
+        }
+    }
+#endif
     if (a.detect) gate.finish(lane, T, a.n_ev + b);
 }
 
