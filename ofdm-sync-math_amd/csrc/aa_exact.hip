@@ -463,10 +463,9 @@ __global__ __launch_bounds__(XW) void rtl_exact_kernel(RtlExactArgs a) {
                   nullptr, a.toff);
 
     // Rows arrive one segment ahead of use: segment g+1's RPS rows are loaded when segment g takes its
-    // own.  gfx9 counts loads and stores on one counter (vmcnt) and they complete out of order, so the
-    // first use of a loaded register waits for EVERY memory operation the wave has in flight
-    // (vmcnt(0)).  A segment therefore takes all its rows at once, before it issues any store, and
-    // its phase-C stores go out after the next segment has taken its rows: the one wait per segment
+    // own.  gfx9 counts loads and stores on one counter (vmcnt), in issue order, so the first use of
+    // a loaded register also waits for every store the wave issued before that load.  A segment
+    // therefore takes all its rows at once, before it issues any store, and its phase-C stores go out after the next segment has taken its rows: the one wait per segment
     // finds only long-issued operations in flight.  (A queue shifted by one row per step waited on
     // every row for the previous row's stores.)
     constexpr int RPS = SEG / RL;

@@ -28,6 +28,9 @@ namespace ofs {
 #ifndef OFS_GATE_FASTFLAGS
 #define OFS_GATE_FASTFLAGS 1
 #endif
+#ifndef OFS_GATE_PRED
+#define OFS_GATE_PRED 0
+#endif
 #ifndef OFS_GATE_NOINLINE_EMIT
 #define OFS_GATE_NOINLINE_EMIT 0
 #endif
@@ -177,6 +180,40 @@ struct AaRowGate {
     __device__ __forceinline__ void row_flags(int lane, int k, int nb, int T, const bool (&ab)[E],
                                               const V (&pm)[E], const V (&pr)[E], const V (&pi)[E],
                                               const V (&m)[E]) {
+#if OFS_GATE_PRED
+        if (FF && DEFER && OFS_GATE_DEFER && Hp >= RL) {
+            // the scan-free machine with the common path predicated: the only branch left per row is
+            // the (rare) gate close; opening, the carry and the per-lane peak tracking are selects
+            int first = GATE_NOKEY, last = -1;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const uint64_t am = __ballot(ab[e]);
+                const int f = am ? E * (int)__builtin_ctzll(am) + e : GATE_NOKEY;
+                const int l = am ? E * (63 - (int)__builtin_clzll(am)) + e : -1;
+                first = min(first, f);
+                last = max(last, l);
+            }
+            const int base = RL * k;
+            const int c = carry_last + Hp;
+            if (carry_last >= 0 && c >= base && c < base + RL && c < T && c - base < first) {
+                accumulate(lane, k, nb, T, gate_open ? 0 : -1, c - base, pm, pr, pi, m);
+                merge();
+                emit(lane, c);
+                gate_open = 0;
+            }
+            const bool has = first != GATE_NOKEY;
+            const bool opens = has && (carry_last < 0 || base + first - 1 - carry_last >= Hp);
+            carry_last = has ? base + last : carry_last;
+            ev_start = opens ? base + first : ev_start;
+            bpm = opens ? (V)-1 : bpm;
+            lv = opens ? (V)-1 : lv;
+            lk = opens ? (RTL ? -1 : ABS_NOKEY) : lk;
+            const int lo = opens ? first : (gate_open ? 0 : RL);    // RL: empty range (gate closed)
+            gate_open = (opens || gate_open) ? 1 : 0;
+            accumulate(lane, k, nb, T, lo, RL - 1, pm, pr, pi, m);
+            return;
+        }
+#endif
         if (FF && OFS_GATE_FASTFLAGS && (OFS_GATE_FFONLY || Hp >= RL)) {
             // hysteresis at least one row: only the row's FIRST above sample can open a gate and
             // only carry_last + Hp can close one (before that first sample), so the machine runs

@@ -465,8 +465,8 @@ __global__ __launch_bounds__(MF_T) void mc_fused_kernel(McArgs a, const double2*
 //   conj(X * H / M) in bit-reversed order (Hbr, as mc_fused_kernel)
 //   inverse DIT  spans 1..16 (same pass), 32..256 (LDS pass), 512..4096 (registers)
 // 4 LDS passes instead of 5, two of them wave-local (no workgroup barrier), each stage's twiddle one
-// product with a per-thread base (bases from a table built once per launch).  gfx9 counts loads and stores on one vmcnt and they complete out of
-// order, so waiting for any load waits for every store in flight: the Hbr slice is loaded right after
+// product with a per-thread base (bases from a table built once per launch).  gfx9 counts loads and stores on one vmcnt, in issue
+// order, so waiting for a load also waits for every store issued before it: the Hbr slice is loaded right after
 // the previous block's stores (waited for in the middle pass, by when those stores have drained), and the
 // next block's input is taken into registers BEFORE this block's stores are issued.
 constexpr int MP_T = 512;

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--same", action="store_true", help="realloc sweep without re-allocating (time variation)")
     ap.add_argument("--contig", action="store_true", help="arena rounds use a physically contiguous arena (bench.py)")
     ap.add_argument("--pre", type=float, default=0.0, help="GiB allocated (and held) before the first round")
+    ap.add_argument("--check", action="store_true", help="realloc: compare every library's events")
     ap.add_argument("--libs", default="", help="comma list of library paths timed on the same buffers (realloc)")
     a = ap.parse_args()
     if a.realloc:
@@ -118,6 +119,17 @@ def realloc_sweep(a):
             torch.cuda.synchronize()
             res[name] = round(e0.elapsed_time(e1) / a.steps, 5)
         res = {n: res[n] for n, _ in libs}
+        if a.check:                              # same events from every library (bit-identical)
+            outs = []
+            for name, lib in libs:
+                n_ev.zero_(); ev_i.fill_(-7); ev_r.fill_(-7.0)
+                lib.ofs_aa_detect(*args)
+                torch.cuda.synchronize()
+                outs.append((n_ev.clone(), ev_i.clone(), ev_r.clone()))
+            res["events"] = int(outs[0][0].sum())
+            res["same"] = all(torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+                              and torch.equal(o[2].view(torch.int64), outs[0][2].view(torch.int64))
+                              for o in outs[1:])
         print(json.dumps({"round": r, "ms": res, "x": hex(x.data_ptr()), "P": hex(P.data_ptr())}), flush=True)
         if not a.same or len(keep) == 0:
             keep.append((x, P, R, M))             # hold: the next round gets new physical pages
