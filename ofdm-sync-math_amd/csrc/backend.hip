@@ -236,6 +236,20 @@ __device__ void load_window(const BeArgs& a, int64_t b, int64_t s, double cfo, d
     lds_barrier();
 }
 
+// the thread index, opaque to the compiler inside the fast kernel's frame loop: values derived from
+// it (addresses, masks, bin indices) are recomputed per frame instead of being hoisted out of the
+// loop and held in registers across it (OFS_BE_REMAT = 0: plain threadIdx.x, A/B)
+#ifndef OFS_BE_REMAT
+#define OFS_BE_REMAT 1
+#endif
+__device__ __forceinline__ int be_tid() {
+    int t = threadIdx.x;
+#if OFS_BE_REMAT
+    asm volatile("" : "+v"(t));
+#endif
+    return t;
+}
+
 template <int FMT> struct BeRaw { using T = float2; };          // the input word kept in registers
 template <> struct BeRaw<OFS_C128> { using T = double2; };
 template <> struct BeRaw<OFS_CI16> { using T = short2; };
@@ -262,7 +276,7 @@ struct BeWindow {
         if (s >= 0 && s + SPT * BW <= a.T) {
 #pragma unroll
             for (int r = 0; r < NBT; ++r) {
-                const T* p = x + (b * NBT + r) * a.T + s + threadIdx.x;
+                const T* p = x + (b * NBT + r) * a.T + s + be_tid();
 #pragma unroll
                 for (int m = 0; m < SPT; ++m) v[r][m] = p[BW * m];
             }
@@ -271,7 +285,7 @@ struct BeWindow {
             for (int r = 0; r < NBT; ++r)
 #pragma unroll
                 for (int m = 0; m < SPT; ++m) {
-                    const int64_t i = s + threadIdx.x + BW * m;
+                    const int64_t i = s + be_tid() + BW * m;
                     v[r][m] = (i >= 0 && i < a.T) ? x[(b * NBT + r) * a.T + i] : zero_raw<T>();
                 }
         }
@@ -287,10 +301,10 @@ struct BeCp {
         const bool full = ps >= 0 && ps + a.N + a.cp <= a.T;
 #pragma unroll
         for (int r = 0; r < NBT; ++r) {
-            const T* p = x + (b * NBT + r) * a.T + ps + threadIdx.x;
+            const T* p = x + (b * NBT + r) * a.T + ps + be_tid();
 #pragma unroll
             for (int m = 0; m < BE_CPT; ++m) {
-                const int n = threadIdx.x + BW * m;
+                const int n = be_tid() + BW * m;
                 const int64_t i0 = ps + n, i1 = ps + a.N + n;
                 const bool ok = !a.cfo_in && n < a.cp && (full || (i0 >= 0 && i1 < a.T));
                 u[r][m] = ok ? p[BW * m] : zero_raw<T>();
@@ -306,14 +320,14 @@ __device__ __forceinline__ void place_window(const BeArgs& a, int64_t s, double 
                                              double2* buf, int LB) {
     const double w0 = 2.0 * M_PI * (-cfo);
     double sn, cs, ss, cc;
-    sincos(w0 * (double)(s + (int64_t)threadIdx.x) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    sincos(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
     sincos(w0 * (double)BW / a.fs, &ss, &cc);
     double2 tone = make_double2(cs, sn);
     const double2 step = make_double2(cc, ss);
-    const int rb = bitrev(threadIdx.x, LB);
+    const int rb = bitrev(be_tid(), LB);
 #pragma unroll
     for (int m = 0; m < SPT; ++m) {
-        const int n = threadIdx.x + BW * m;
+        const int n = be_tid() + BW * m;
         const int64_t i = s + n;
         double2 acc = make_double2(0.0, 0.0);
         if (i >= 0 && i < a.T) {
@@ -397,7 +411,7 @@ __device__ void fft_lds_q(double2* buf, const double2* twq, int N, int LB) {
 // BW/64 wave totals through LDS; every thread gets the NV results.
 template <int NV>
 __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = be_tid() & 63, w = be_tid() >> 6;
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = ofs::readlane(ofs::wave_scan_add(v[i], lane), 63);
     lds_barrier();                                           // red's previous readers are done
@@ -421,7 +435,7 @@ __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
 __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U, double kmean, double skz, double den,
                                     double* red, double* scan_tot) {
     const int per = (U + BW - 1) / BW;
-    const int u0 = threadIdx.x * per, u1 = min(U, u0 + per);
+    const int u0 = be_tid() * per, u1 = min(U, u0 + per);
     double local = 0.0;
     for (int u = max(u0, 1); u < u1; ++u) {
         const double dd = ph[u] - ph[u - 1];
@@ -431,7 +445,7 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
             local += dm - dd;
         }
     }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = be_tid() & 63, w = be_tid() >> 6;
     const double incl = ofs::wave_scan_add(local, lane);
     if (lane == 63) scan_tot[w] = incl;
     lds_barrier();
@@ -463,25 +477,56 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
 #define OFS_BE_MINWG 2             // workgroups per CU the register budget is cut for (r03s: 2 beats
                                    // 3 - 1.21 vs 1.29 ms - the 168-VGPR cut spills)
 #endif
+// LDS layout of the fast kernel's sample buffer and quarter twiddle table: both are stored with an
+// XOR swizzle of the element index, so the window placement, the radix-8/8/4 passes and their
+// twiddle reads are free of bank conflicts.  Identity layout: SQ_LDS_BANK_CONFLICT was 60 % of the
+// kernel's LDS cycles (r05w); tools/lds_banks.py models every access (SPT 8: 5056 -> 1728 LDS
+// cycles per FFT and workgroup, the conflict-free count).  Both swizzles are linear over XOR, so
+// swz(p | i·h) = swz(p) ^ swz(i·h) for disjoint bit sets: a per-thread base XOR a constant.
+#ifndef OFS_BE_SWZ
+#define OFS_BE_SWZ 1               // 0: identity layout (A/B)
+#endif
+template <int SPT>
+__device__ __forceinline__ constexpr int bsw(int e) {
+    constexpr int LS = __builtin_ctz(SPT);
+    return OFS_BE_SWZ ? e ^ ((e >> (LS + 5)) & 7) ^ (((e >> (LS + 3)) & 3) << LS) : e;
+}
+__device__ __forceinline__ constexpr int tsw(int j) { return OFS_BE_SWZ ? j ^ (((j >> 4) ^ (j >> 8)) & 15) : j; }
+
+// w^j for 0 <= j < N/2 from the swizzled quarter table, given as the swizzled index of j mod N/4
+// and j's quadrant bit: w^{j} = -i·w^{j-N/4}
+__device__ __forceinline__ double2 twq_sw(const double2* twq, int ti, bool upper) {
+    const double2 v = twq[ti];
+    return upper ? make_double2(v.y, -v.x) : v;
+}
+
 // Radix-R DIT pass over groups of R·h (R = 2, 4, 8: log2 R radix-2 stages in registers): thread j
 // takes the R elements p + i·h of group g = j / h, k = j mod h, and applies the stages of spans h,
 // 2h, ... with the twiddles w^{(k + q·h)·N/(2·span)} - exactly the radix-2 stages' operations in
 // their order (bit-identical to fft_lds), one LDS round trip and one barrier per log2 R stages.
-template <int R>
-__device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int N, int h) {
-    const int Q = N / 4;
-    for (int j = threadIdx.x; j < N / R; j += BW) {
+// p and i·h have disjoint bits, as have k·str and q·h·str (k < h), so every address is a
+// per-thread swizzled base XOR a compile-time constant.
+template <int R, int SPT>
+__device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int h) {
+    constexpr int N = SPT * BW, Q = N / 4, LQ = __builtin_ctz(Q);
+    for (int j = be_tid(); j < N / R; j += BW) {
         const int g = j / h, k = j - g * h;
-        const int p = g * R * h + k;
+        const int pb = bsw<SPT>(g * R * h + k);
         double2 v[R];
 #pragma unroll
-        for (int i = 0; i < R; ++i) v[i] = buf[p + i * h];
+        for (int i = 0; i < R; ++i) v[i] = buf[pb ^ bsw<SPT>(i * h)];
 #pragma unroll
         for (int sp = 1; sp < R; sp <<= 1) {
             const int str = N / (2 * sp * h);
+            const int kk = k * str;                                   // < N / (2·sp)
+            const int tb = tsw(kk & (Q - 1));
+            const bool up = (kk >> LQ) & 1;
             double2 w[R / 2];
 #pragma unroll
-            for (int q = 0; q < sp; ++q) w[q] = twq_at(twq, (k + q * h) * str, Q);
+            for (int q = 0; q < sp; ++q) {
+                const int qq = q * (N / (2 * sp));
+                w[q] = twq_sw(twq, tb ^ tsw(qq & (Q - 1)), up != (bool)((qq >> LQ) & 1));
+            }
 #pragma unroll
             for (int i0 = 0; i0 < R; i0 += 2 * sp)
 #pragma unroll
@@ -492,7 +537,7 @@ __device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int N
                 }
         }
 #pragma unroll
-        for (int i = 0; i < R; ++i) buf[p + i * h] = v[i];
+        for (int i = 0; i < R; ++i) buf[pb ^ bsw<SPT>(i * h)] = v[i];
     }
     lds_barrier();
 }
@@ -517,14 +562,14 @@ __device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, dou
     constexpr int N = SPT * BW, LS = Log2<SPT>::value;
     const double w0 = 2.0 * M_PI * (-cfo);
     double sn, cs, ss, cc;
-    sincos(w0 * (double)(s + (int64_t)threadIdx.x) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    sincos(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
     sincos(w0 * (double)BW / a.fs, &ss, &cc);
     double2 tone = make_double2(cs, sn);
     const double2 step = make_double2(cc, ss);
     double2 v[SPT];
 #pragma unroll
     for (int m = 0; m < SPT; ++m) {
-        const int64_t i = s + threadIdx.x + BW * m;
+        const int64_t i = s + be_tid() + BW * m;
         double2 acc = make_double2(0.0, 0.0);
         if (i >= 0 && i < a.T) {
 #pragma unroll
@@ -543,24 +588,24 @@ __device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, dou
         for (int i0 = 0; i0 < SPT; i0 += 2 * sp)
 #pragma unroll
             for (int q = 0; q < sp; ++q) {
-                const double2 w = twq_at(twq, q * (N / (2 * sp)), N / 4);
+                const int qq = q * (N / (2 * sp));
+                const double2 w = twq_sw(twq, tsw(qq & (N / 4 - 1)), qq >= N / 4);
                 const double2 t = cmul(w, v[i0 + q + sp]), u = v[i0 + q];
                 v[i0 + q] = make_double2(u.x + t.x, u.y + t.y);
                 v[i0 + q + sp] = make_double2(u.x - t.x, u.y - t.y);
             }
     }
-    double2* dst = buf + bitrev(threadIdx.x, 8) * SPT;
+    const int db = bsw<SPT>(bitrev(be_tid(), 8) * SPT);                  // bsw(i) = i for i < SPT
 #pragma unroll
-    for (int i = 0; i < SPT; ++i) dst[i] = v[i];
+    for (int i = 0; i < SPT; ++i) buf[db ^ i] = v[i];
     lds_barrier();
 }
 
 template <int SPT>
 __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
-    constexpr int N = SPT * BW;
-    fft_pass<8>(buf, twq, N, SPT);
-    fft_pass<8>(buf, twq, N, 8 * SPT);
-    fft_pass<4>(buf, twq, N, 64 * SPT);
+    fft_pass<8, SPT>(buf, twq, SPT);
+    fft_pass<8, SPT>(buf, twq, 8 * SPT);
+    fft_pass<4, SPT>(buf, twq, 64 * SPT);
 }
 
 #ifndef OFS_BE_PF
@@ -589,7 +634,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     for (int j = threadIdx.x; j < N / 4; j += BW) {
         double sn, cs;
         sincospi(-2.0 * (double)j / (double)N, &sn, &cs);
-        twq[j] = make_double2(cs, sn);
+        twq[R8 ? tsw(j) : j] = make_double2(cs, sn);
     }
     int kb[UPT];                              // this thread's used bins u = tid + BW·j, as X indices
     double bsum[1] = {0.0};
@@ -597,7 +642,8 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     for (int j = 0; j < UPT; ++j) {
         const int u = threadIdx.x + BW * j;
         int k = u < U ? a.bins[u] % N : 0;
-        kb[j] = k < 0 ? k + N : k;
+        k = k < 0 ? k + N : k;
+        kb[j] = R8 ? bsw<SPT>(k) : k;                                     // buffer slot of bin k
         if (u < U) bsum[0] += (double)a.bins[u];
     }
     // the phase-slope fit's frame-invariant sums (np.mean(k), Σ kz, Σ kz² + 1e-12)
@@ -644,7 +690,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
         block_sums<2>(pp, red);
         cfo = -atan2(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
     }
-    if (a.cfo_out && threadIdx.x == 0) a.cfo_out[b] = cfo;
+    if (a.cfo_out && be_tid() == 0) a.cfo_out[b] = cfo;
     const double2* pil = a.pilot + b * a.pilot_stride;
     const double2* dat = a.data + b * a.data_stride;
     BE_T(0)
@@ -662,7 +708,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     double2 hx[UPT];                                                  // h, later xhat
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
-        const int u = threadIdx.x + BW * j;
+        const int u = be_tid() + BW * j;
         hx[j] = make_double2(0.0, 0.0);
         if (u < U) {
             const double2 p = pil[u];
@@ -675,7 +721,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     lds_barrier();
     BE_T(3)
     const double slope = unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, red, scan_tot);
-    if (threadIdx.x == 0) {
+    if (be_tid() == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
         if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
     }
@@ -699,7 +745,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     double gs[4] = {0.0, 0.0, 0.0, 0.0};                              // vdot(xhat, ref), |xhat|², |ref|²
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
-        const int u = threadIdx.x + BW * j;
+        const int u = be_tid() + BW * j;
         if (u < U) {
             const double2 h = hx[j];
             const double2 xh = cdiv(buf[kb[j]], make_double2(h.x + 1e-9, h.y));   // equalize
@@ -718,7 +764,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     double ee[1] = {0.0};
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
-        const int u = threadIdx.x + BW * j;
+        const int u = be_tid() + BW * j;
         if (u < U) {
             const double2 xa = cmul(hx[j], g);
             if (a.xa_out) a.xa_out[b * U + u] = xa;
@@ -728,7 +774,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
         }
     }
     block_sums<1>(ee, red);
-    if (threadIdx.x == 0) {
+    if (be_tid() == 0) {
         const double evm = sqrt((ee[0] / (double)U) / (rr / (double)U));
         if (a.gain_out) a.gain_out[b] = g;
         if (a.evm_out) a.evm_out[b] = evm;
@@ -737,7 +783,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     BE_T(8)
     }
 #if OFS_BE_TIMING
-    if (threadIdx.x == 0)
+    if (be_tid() == 0)
         for (int i = 0; i < 9; ++i) atomicAdd(&be_prof[i], (unsigned long long)tacc[i]);
 #endif
 }
