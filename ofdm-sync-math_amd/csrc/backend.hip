@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include "ofdmsync.h"
 #include "ofs_common.h"
+#include "be_math.h"
 
 namespace {
 
@@ -320,8 +321,8 @@ __device__ __forceinline__ void place_window(const BeArgs& a, int64_t s, double 
                                              double2* buf, int LB) {
     const double w0 = 2.0 * M_PI * (-cfo);
     double sn, cs, ss, cc;
-    sincos(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
-    sincos(w0 * (double)BW / a.fs, &ss, &cc);
+    ofs_bemath::sincos_lean(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    ofs_bemath::sincos_lean(w0 * (double)BW / a.fs, &ss, &cc);
     double2 tone = make_double2(cs, sn);
     const double2 step = make_double2(cc, ss);
     const int rb = bitrev(be_tid(), LB);
@@ -474,8 +475,10 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
 }
 
 #ifndef OFS_BE_MINWG
-#define OFS_BE_MINWG 2             // workgroups per CU the register budget is cut for (r03s: 2 beats
-                                   // 3 - 1.21 vs 1.29 ms - the 168-VGPR cut spills)
+#define OFS_BE_MINWG 3             // workgroups per CU the register budget is cut for (168 VGPRs; LDS
+                                   // 50 KB each).  r05ab: with the lean atan2 / sincos (be_math.h) the
+                                   // kernel needs 133 VGPRs, so 3 fit: 0.94 -> 0.82 ms.  (Round 3, with
+                                   // ocml's: 2 beat 3, 1.21 vs 1.29 ms - the 168-VGPR cut spilled.)
 #endif
 // LDS layout of the fast kernel's sample buffer and quarter twiddle table: both are stored with an
 // XOR swizzle of the element index, so the window placement, the radix-8/8/4 passes and their
@@ -562,8 +565,8 @@ __device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, dou
     constexpr int N = SPT * BW, LS = Log2<SPT>::value;
     const double w0 = 2.0 * M_PI * (-cfo);
     double sn, cs, ss, cc;
-    sincos(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
-    sincos(w0 * (double)BW / a.fs, &ss, &cc);
+    ofs_bemath::sincos_lean(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
+    ofs_bemath::sincos_lean(w0 * (double)BW / a.fs, &ss, &cc);
     double2 tone = make_double2(cs, sn);
     const double2 step = make_double2(cc, ss);
     double2 v[SPT];
@@ -609,7 +612,12 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 }
 
 #ifndef OFS_BE_PF
-#define OFS_BE_PF 1                // 0: each frame's pilot window / CP loads issued at its start (A/B)
+#define OFS_BE_PF 0                // 1: the next frame's pilot window / CP loads issued during this frame's
+                                   // data phase (round 3, 0.97 vs 1.00 ms at 2 workgroups per CU; at 3:
+                                   // 0.820 vs 0.823 ms with 8 VGPR spills, r05ab - off)
+#endif
+#ifndef OFS_BE_DEARLY
+#define OFS_BE_DEARLY 0
 #endif
 #ifndef OFS_BE_R8
 #define OFS_BE_R8 1                // 0: place_window + fft_lds_q (A/B)
@@ -663,6 +671,10 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     const double skz = kst[0], kden = kst[1] + 1e-12;
     BeWindow<FMT, SPT, NBT> pwin;
     BeCp<FMT, NBT> cpx;
+    // the data window's loads: issued right after the pilot window is placed (DEARLY: their HBM
+    // latency hides under the pilot FFT, LS and unwrap; 32 VGPRs held meanwhile) or just before use
+    constexpr bool DEARLY = OFS_BE_DEARLY && R8;
+    BeWindow<FMT, SPT, NBT> dwin;
     if (PF && blockIdx.x < a.B) {
         pwin.issue(a, blockIdx.x, a.pilot_start[blockIdx.x] + a.cp);
         cpx.issue(a, blockIdx.x, a.pilot_start[blockIdx.x]);
@@ -688,7 +700,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
                 pp[1] += u.y * v.x - u.x * v.y;
             }
         block_sums<2>(pp, red);
-        cfo = -atan2(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
+        cfo = -ofs_bemath::atan2_lean(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
     }
     if (a.cfo_out && be_tid() == 0) a.cfo_out[b] = cfo;
     const double2* pil = a.pilot + b * a.pilot_stride;
@@ -697,6 +709,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     // ---- pilot: FFT, used bins, LS estimate ----
     if constexpr (R8) {
         place_window_fft<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, twq);
+        if constexpr (DEARLY) dwin.issue(a, b, ds + a.cp);
         BE_T(1)
         fft_rest<SPT>(buf, twq);
     } else {
@@ -714,7 +727,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
             const double2 p = pil[u];
             const double2 h = cdiv(buf[kb[j]], make_double2(p.x + 1e-9, p.y));   // y / (x + eps)
             hx[j] = h;
-            ph[u] = atan2(h.y, h.x);
+            ph[u] = ofs_bemath::atan2_lean(h.y, h.x);
             if (a.h_out) a.h_out[b * U + u] = h;
         }
     }
@@ -728,8 +741,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     BE_T(4)
     // ---- data: FFT, equalise, complex-gain alignment, EVM ----
     {
-        BeWindow<FMT, SPT, NBT> dwin;                                 // (issued during the pilot's work instead:
-        dwin.issue(a, b, ds + a.cp);                                  // r03w, 1.00 vs 0.97 ms - registers)
+        if constexpr (!DEARLY) dwin.issue(a, b, ds + a.cp);
         if constexpr (R8) place_window_fft<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, twq);
         else place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
     }
