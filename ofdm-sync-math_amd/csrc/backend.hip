@@ -354,7 +354,9 @@ __device__ __forceinline__ void place_window(const BeArgs& a, int64_t s, double 
 //    bins u = t + BW·j in the LS, EQ and EVM loops alike, so only the phases (unwrap: cross-bin)
 //    go to LDS;
 //  * the twiddle table holds N/4 entries (w^{j+N/4} = -i·w^j);
-// so a workgroup needs N·16 + N/4·16 + n_used·8 bytes of LDS (50 KB at N = 2048): 3 per CU.
+// so a workgroup needs N·16 + N/4·16 bytes of LDS (40 KB at N = 2048, the phases and reduction
+// slots overlaying the sample buffer: OFS_BE_LDS40) and, with be_math.h's lean atan2 / sincos,
+// 128 VGPRs: 4 workgroups (16 waves) per CU.
 // variant BE_FAST=0 selects the generic kernel (A/B).
 #ifndef OFS_BE_TIMING
 #define OFS_BE_TIMING 0            // diagnostic builds: per-phase cycles (tools/be_phase.py)
@@ -475,10 +477,11 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
 }
 
 #ifndef OFS_BE_MINWG
-#define OFS_BE_MINWG 3             // workgroups per CU the register budget is cut for (168 VGPRs; LDS
-                                   // 50 KB each).  r05ab: with the lean atan2 / sincos (be_math.h) the
-                                   // kernel needs 133 VGPRs, so 3 fit: 0.94 -> 0.82 ms.  (Round 3, with
-                                   // ocml's: 2 beat 3, 1.21 vs 1.29 ms - the 168-VGPR cut spilled.)
+#define OFS_BE_MINWG 4             // workgroups per CU the register budget is cut for (128 VGPRs, with
+                                   // the 40 KB LDS layout, OFS_BE_LDS40).  r05ab: with the lean atan2 /
+                                   // sincos (be_math.h) the kernel needs 133 VGPRs, so 3 fit (0.94 ->
+                                   // 0.82 ms); r05ad: 4 at 127 VGPRs (4 spilled), 0.826 -> 0.755 ms, bit-
+                                   // identical.  (Round 3, with ocml's: 2 beat 3, 1.21 vs 1.29 ms.)
 #endif
 // LDS layout of the fast kernel's sample buffer and quarter twiddle table: both are stored with an
 // XOR swizzle of the element index, so the window placement, the radix-8/8/4 passes and their
@@ -616,6 +619,9 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
                                    // data phase (round 3, 0.97 vs 1.00 ms at 2 workgroups per CU; at 3:
                                    // 0.820 vs 0.823 ms with 8 VGPR spills, r05ab - off)
 #endif
+#ifndef OFS_BE_LDS40
+#define OFS_BE_LDS40 1             // phases and reduction slots inside the sample buffer (0: own LDS, A/B)
+#endif
 #ifndef OFS_BE_DEARLY
 #define OFS_BE_DEARLY 0
 #endif
@@ -630,12 +636,23 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     long long tprev = __builtin_amdgcn_s_memtime();
 #endif
     extern __shared__ __attribute__((aligned(16))) double2 bsm[];
-    __shared__ double red[4 * (BW / 64)];
-    __shared__ double scan_tot[BW / 64];
     constexpr int N = SPT * BW;
     double2* buf = bsm;                       // N
     double2* twq = bsm + N;                   // N / 4
+#if OFS_BE_LDS40
+    // LDS = the sample buffer and the twiddle table only (40 KB at N = 2048: 4 workgroups per CU):
+    // the phases live in the buffer between the pilot's LS and the unwrap (the pilot spectrum is in
+    // registers by then), the reduction slots at its end; barriers before each window placement
+    // keep the placement's writes behind the last reads of those slots
+    double* ph = reinterpret_cast<double*>(buf);                       // n_used <= 2N - 5·BW/64
+    double* red = reinterpret_cast<double*>(buf) + 2 * N - 5 * (BW / 64);
+    double* scan_tot = red + 4 * (BW / 64);
+#else
+    __shared__ double red[4 * (BW / 64)];
+    __shared__ double scan_tot[BW / 64];
     double* ph = reinterpret_cast<double*>(twq + N / 4);   // n_used: phase / unwrap
+#endif
+    constexpr bool L40 = OFS_BE_LDS40;
     const int U = a.n_used, LB = 31 - __clz(N);
     constexpr bool R8 = OFS_BE_R8 && SPT <= 8;           // 16 samples per thread in registers would spill
     constexpr bool PF = OFS_BE_PF && SPT <= 8 && sizeof(typename BeRaw<FMT>::T) <= 8;   // (complex128 too)
@@ -707,6 +724,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     const double2* dat = a.data + b * a.data_stride;
     BE_T(0)
     // ---- pilot: FFT, used bins, LS estimate ----
+    if constexpr (L40) lds_barrier();                                 // the CFO sums' slots are read
     if constexpr (R8) {
         place_window_fft<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, twq);
         if constexpr (DEARLY) dwin.issue(a, b, ds + a.cp);
@@ -727,8 +745,16 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
             const double2 p = pil[u];
             const double2 h = cdiv(buf[kb[j]], make_double2(p.x + 1e-9, p.y));   // y / (x + eps)
             hx[j] = h;
-            ph[u] = ofs_bemath::atan2_lean(h.y, h.x);
+            if constexpr (!L40) ph[u] = ofs_bemath::atan2_lean(h.y, h.x);
             if (a.h_out) a.h_out[b * U + u] = h;
+        }
+    }
+    if constexpr (L40) {                                              // ph overlays the pilot spectrum
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < UPT; ++j) {
+            const int u = be_tid() + BW * j;
+            if (u < U) ph[u] = ofs_bemath::atan2_lean(hx[j].y, hx[j].x);
         }
     }
     lds_barrier();
@@ -742,6 +768,7 @@ __global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArg
     // ---- data: FFT, equalise, complex-gain alignment, EVM ----
     {
         if constexpr (!DEARLY) dwin.issue(a, b, ds + a.cp);
+        if constexpr (L40) lds_barrier();                             // the fit sums' slots are read
         if constexpr (R8) place_window_fft<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, twq);
         else place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
     }
@@ -936,7 +963,7 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
                       ((n_fft == 4 * BW && n_used <= 3 * BW) || (n_fft == 8 * BW && n_used <= 5 * BW) ||
                        (n_fft == 16 * BW && n_used <= 10 * BW));
     if (fast) {
-        const size_t lds_f = (size_t)n_fft * 16 + (size_t)(n_fft / 4) * 16 + (size_t)n_used * 8;
+        const size_t lds_f = (size_t)n_fft * 16 + (size_t)(n_fft / 4) * 16 + (OFS_BE_LDS40 ? 0 : (size_t)n_used * 8);
         auto launch_f = [&](auto kern) -> int32_t {
             if (lds_f > 64 * 1024 &&
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
