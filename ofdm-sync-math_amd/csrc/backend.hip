@@ -629,8 +629,9 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 #define OFS_BE_R8 1                // 0: place_window + fft_lds_q (A/B)
 #endif
 
+// (N = 4096: 80 KB of LDS, 2 workgroups per CU whatever the registers - so their budget is 256)
 template <int FMT, int SPT, int NBT, int UPT>
-__global__ __launch_bounds__(BW, OFS_BE_MINWG) void rx_backend_fast_kernel(BeArgs a) {
+__global__ __launch_bounds__(BW, SPT >= 16 ? 2 : OFS_BE_MINWG) void rx_backend_fast_kernel(BeArgs a) {
 #if OFS_BE_TIMING
     long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = __builtin_amdgcn_s_memtime();
