@@ -410,17 +410,31 @@ __device__ void fft_lds_q(double2* buf, const double2* twq, int N, int LB) {
     }
 }
 
+#ifndef OFS_BE_ZSCAN
+#define OFS_BE_ZSCAN 1             // block sums by the zero-filled DPP ladder (0: predicated ladder, A/B)
+#endif
 // NV block-wide sums with one pair of barriers: DPP wave sums (inclusive scan, lane 63), then the
 // BW/64 wave totals through LDS; every thread gets the NV results.
 template <int NV>
 __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
     const int lane = be_tid() & 63, w = be_tid() >> 6;
+#if OFS_BE_ZSCAN
+    // zero-filled DPP ladder (no lane predicates; the same additions in the same order), the wave
+    // total written by lane 63 itself (no readlane)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = ofs::scan_add(v[i]);
+    lds_barrier();                                           // red's previous readers are done
+    if (lane == 63)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
+#else
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = ofs::readlane(ofs::wave_scan_add(v[i], lane), 63);
     lds_barrier();                                           // red's previous readers are done
     if (lane == 0)
 #pragma unroll
         for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
+#endif
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -449,7 +463,7 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
         }
     }
     const int lane = be_tid() & 63, w = be_tid() >> 6;
-    const double incl = ofs::wave_scan_add(local, lane);
+    const double incl = OFS_BE_ZSCAN ? ofs::scan_add(local) : ofs::wave_scan_add(local, lane);
     if (lane == 63) scan_tot[w] = incl;
     lds_barrier();
     double run = incl - local;
