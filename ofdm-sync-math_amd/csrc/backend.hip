@@ -251,6 +251,10 @@ __device__ __forceinline__ int be_tid() {
     return t;
 }
 
+// log10 for the per-frame EVM in dB (one lane per frame): out of line, so that ocml's coefficients
+// are not hoisted out of the fast kernel's frame loop into registers held across it
+__device__ __attribute__((noinline)) double be_log10(double x) { return log10(x); }
+
 template <int FMT> struct BeRaw { using T = float2; };          // the input word kept in registers
 template <> struct BeRaw<OFS_C128> { using T = double2; };
 template <> struct BeRaw<OFS_CI16> { using T = short2; };
@@ -832,7 +836,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : OFS_BE_MINWG) void rx_backend_f
         const double evm = sqrt((ee[0] / (double)U) / (rr / (double)U));
         if (a.gain_out) a.gain_out[b] = g;
         if (a.evm_out) a.evm_out[b] = evm;
-        if (a.evm_db_out) a.evm_db_out[b] = 20.0 * log10(evm + 1e-12);
+        if (a.evm_db_out) a.evm_db_out[b] = 20.0 * be_log10(evm + 1e-12);
     }
     BE_T(8)
     }

@@ -26,15 +26,22 @@ namespace ofs_bemath {
 using std::fabs; using std::floor; using std::fma; using std::rint; using std::signbit;
 #endif
 
-// an fp64 constant materialised into a scalar register pair where it is used: without this the
-// compiler hoists every coefficient out of the kernel's frame loop into a VGPR pair held across it
-// (r05ab: ~50 VGPRs of polynomial coefficients)
-OFS_HD inline double K(double c) {
+// an fp64 constant materialised into scalar registers by the instructions at its use: without this
+// the compiler hoists every coefficient out of the kernel's frame loop into a VGPR pair held across
+// it (r05ab: ~50 VGPRs of polynomial coefficients), and with the materialisation outside the asm it
+// hoists the scalar moves instead and spills the SGPRs to VGPR lanes (a v_readlane per use)
 #if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("" : "+s"(c));
-#endif
-    return c;
+template <unsigned long long B>
+__device__ __forceinline__ double kd_() {
+    unsigned lo, hi;
+    asm volatile("s_mov_b32 %0, %2\n\ts_mov_b32 %1, %3"
+                 : "=s"(lo), "=s"(hi) : "i"((unsigned)(B & 0xffffffffu)), "i"((unsigned)(B >> 32)));
+    return __hiloint2double((int)hi, (int)lo);
 }
+#define K(c) ofs_bemath::kd_<__builtin_bit_cast(unsigned long long, (double)(c))>()
+#else
+#define K(c) (c)
+#endif
 
 OFS_HD inline void sincos_lean(double x, double* s, double* c) {
     const double n = rint(x * K(0.63661977236758134308));             // 2/pi
