@@ -39,8 +39,17 @@ __device__ __forceinline__ double kd_() {
     return __hiloint2double((int)hi, (int)lo);
 }
 #define K(c) ofs_bemath::kd_<__builtin_bit_cast(unsigned long long, (double)(c))>()
+// a·b + c with the constant c read from its scalar pair by the VOP3 form: the compiler otherwise
+// picks v_fmac_f64, whose addend is the destination, and copies every constant into VGPRs first
+// (two v_mov_b32 per Horner step)
+__device__ __forceinline__ double fmak(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
 #else
 #define K(c) (c)
+inline double fmak(double a, double b, double c) { return fma(a, b, c); }
 #endif
 
 OFS_HD inline void sincos_lean(double x, double* s, double* c) {
@@ -50,15 +59,15 @@ OFS_HD inline void sincos_lean(double x, double* s, double* c) {
     r = fma(-n, K(-1.4973849048591698e-33), r);
     const double z = r * r;
     double ps = fma(z, K(1.58969099521155010221e-10), K(-2.50507602534068634195e-08));
-    ps = fma(z, ps, K(2.75573137070700676789e-06));
-    ps = fma(z, ps, K(-1.98412698298579493134e-04));
-    ps = fma(z, ps, K(8.33333333332248946124e-03));
-    const double sn = r + (z * r) * fma(z, ps, K(-1.66666666666666324348e-01));
+    ps = fmak(z, ps, K(2.75573137070700676789e-06));
+    ps = fmak(z, ps, K(-1.98412698298579493134e-04));
+    ps = fmak(z, ps, K(8.33333333332248946124e-03));
+    const double sn = r + (z * r) * fmak(z, ps, K(-1.66666666666666324348e-01));
     double pc = fma(z, K(-1.13596475577881948265e-11), K(2.08757232129817482790e-09));
-    pc = fma(z, pc, K(-2.75573143513906633035e-07));
-    pc = fma(z, pc, K(2.48015872894767294178e-05));
-    pc = fma(z, pc, K(-1.38888888888741095749e-03));
-    pc = z * fma(z, pc, K(4.16666666666666019037e-02));
+    pc = fmak(z, pc, K(-2.75573143513906633035e-07));
+    pc = fmak(z, pc, K(2.48015872894767294178e-05));
+    pc = fmak(z, pc, K(-1.38888888888741095749e-03));
+    pc = z * fmak(z, pc, K(4.16666666666666019037e-02));
     const double hz = 0.5 * z, w = 1.0 - hz;
     const double cn = w + (((1.0 - w) - hz) + z * pc);
     const double q = n - 4.0 * floor(n * 0.25);                       // quadrant 0..3 (exact)
@@ -78,14 +87,14 @@ OFS_HD inline double atan2_lean(double y, double x) {
     const double dd = den == 0.0 ? 1.0 : (r0 ? den : (r1 ? 2.0 * den + num : num + den));
     const double z = nn / dd, z2 = z * z, w = z2 * z2;
     double s1 = fma(w, K(1.62858201153657823623e-02), K(4.97687799461593236017e-02));
-    s1 = fma(w, s1, K(6.66107313738753120669e-02));
-    s1 = fma(w, s1, K(9.09088713343650656196e-02));
-    s1 = fma(w, s1, K(1.42857142725034663711e-01));
-    s1 = z2 * fma(w, s1, K(3.33333333333329318027e-01));
+    s1 = fmak(w, s1, K(6.66107313738753120669e-02));
+    s1 = fmak(w, s1, K(9.09088713343650656196e-02));
+    s1 = fmak(w, s1, K(1.42857142725034663711e-01));
+    s1 = z2 * fmak(w, s1, K(3.33333333333329318027e-01));
     double s2 = fma(w, K(-3.65315727442169155270e-02), K(-5.83357013379057348645e-02));
-    s2 = fma(w, s2, K(-7.69187620504482999495e-02));
-    s2 = fma(w, s2, K(-1.11111104054623557880e-01));
-    s2 = w * fma(w, s2, K(-1.99999999998764832476e-01));
+    s2 = fmak(w, s2, K(-7.69187620504482999495e-02));
+    s2 = fmak(w, s2, K(-1.11111104054623557880e-01));
+    s2 = w * fmak(w, s2, K(-1.99999999998764832476e-01));
     const double zs = z * (s1 + s2);
     const double hi = r1 ? K(4.63647609000806093515e-01) : K(7.85398163397448278999e-01);
     const double lo = r1 ? K(2.26987774529616870924e-17) : K(3.06161699786838301793e-17);
