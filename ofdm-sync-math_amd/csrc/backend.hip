@@ -637,6 +637,10 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
                                    // data phase (round 3, 0.97 vs 1.00 ms at 2 workgroups per CU; at 3:
                                    // 0.820 vs 0.823 ms with 8 VGPR spills, r05ab - off)
 #endif
+#ifndef OFS_BE_MINWG4
+#define OFS_BE_MINWG4 5            // N = 1024 (20 KB of LDS): 5 (96 VGPRs, 4 spilled) 0.823 vs 4: 0.877 ms,
+                                   // 6 (80 VGPRs): 0.827 (r05ak)
+#endif
 #ifndef OFS_BE_LDS40
 #define OFS_BE_LDS40 1             // phases and reduction slots inside the sample buffer (0: own LDS, A/B)
 #endif
@@ -649,7 +653,7 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 
 // (N = 4096: 80 KB of LDS, 2 workgroups per CU whatever the registers - so their budget is 256)
 template <int FMT, int SPT, int NBT, int UPT>
-__global__ __launch_bounds__(BW, SPT >= 16 ? 2 : OFS_BE_MINWG) void rx_backend_fast_kernel(BeArgs a) {
+__global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS_BE_MINWG)) void rx_backend_fast_kernel(BeArgs a) {
 #if OFS_BE_TIMING
     long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     long long tprev = __builtin_amdgcn_s_memtime();

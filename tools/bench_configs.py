@@ -245,15 +245,15 @@ def cfg5(dev, st, steps, warmup, n_seq=1 << 20, seed=5):
                 bytes_per_sample="8 in + 4|8 B per sequence out")
 
 
-def backend(dev, st, steps, warmup):
+def backend(dev, st, steps, warmup, B=16384, N=2048, n_used=1200, name="backend"):
     """Receiver back-end (sc.py:274-311 chain) over a batch of frames: 2 branches, N = 2048,
-    CP = 512, c64 input; CP CFO, two 2048-point FFTs, LS, phase-slope STO, EQ, EVM per frame."""
+    CP = min(N/4, 512), c64 input; CP CFO, two N-point FFTs, LS, phase-slope STO, EQ, EVM per frame."""
     from ofdm_sync_amd import core
-    B, nb, N, cp = 16384, 2, 2048, 512
+    nb, cp = 2, min(N // 4, 512)                                # the fast kernel's cp <= 512
     T = 2 * (N + cp) + 64
     g = torch.Generator(device=dev).manual_seed(11)
     x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
-    k = core.centered_subcarrier_indices(1200)
+    k = core.centered_subcarrier_indices(n_used)
     U = k.size
     ps = torch.full((B,), 32, dtype=torch.int64, device=dev)
     ds = ps + N + cp
@@ -275,9 +275,9 @@ def backend(dev, st, steps, warmup):
     # fit (~12), vdot / EVM sums and the gain product (~20)
     lg = int(np.log2(N))
     flops = 8 * cp * nb + 2 * (N * nb * 8 + N * 6) + 2 * 5 * N * lg + U * (11 + 11 + 12 + 20)
-    return _flops(dict(config="backend",
+    return _flops(dict(config=name,
                        workload=f"receiver back-end, {B} frames x {nb} branches, N={N}, CP={cp}, c64 in, fp64",
-                       kernel="rx_backend_kernel (LDS radix-2 FFTs, one workgroup per frame)", samples=B * nb * 2 * N,
+                       kernel=f"rx_backend_fast_kernel<SPT={N // 256}> (LDS FFTs, one workgroup per frame)", samples=B * nb * 2 * N,
                        ms=ms, alg_bytes=nbytes, bytes_per_sample="windows read once (8 B) + 2 x 16 B per used bin out",
                        frames_per_s=round(B / (ms / 1e3), 1), flops_per_frame=flops), B * flops, "fp64")
 
@@ -680,7 +680,9 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
            "cfg5_rocfft_chunked": lambda *a, **k: cfg5_rocfft(*a, pruned=False, chunked=True, **k),
            "cfg2a_cp12": lambda *a, **k: cfg2a(*a, cp12=True, **k),
            "cfg2b_cp12": lambda *a, **k: cfg2b(*a, cp12=True, **k), "cfg3_T4096": cfg3_T4096, "aa_refshape_c64": aa_refshape_c64, "aa_refshape_c128": aa_refshape_c128,
-"cfg2a": cfg2a, "cfg3": cfg3, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend}
+"cfg2a": cfg2a, "cfg3": cfg3, "cfg3_2ant": cfg3_2ant, "cfg4_2br": cfg4_2br, "cfg3_fp64": cfg3_fp64, "cfg2b": cfg2b, "cfg4": cfg4, "cfg5": cfg5, "cfg5_rocfft": cfg5_rocfft, "cfg3_detect": cfg3_detect, "cfg3_pcie": cfg3_pcie, "backend": backend,
+"backend_n1024": lambda d, s_, k, w: backend(d, s_, k, w, B=32768, N=1024, n_used=600, name="backend_n1024"),
+"backend_n4096": lambda d, s_, k, w: backend(d, s_, k, w, B=8192, N=4096, n_used=2400, name="backend_n4096")}
 
 
 def _selftest_config(name):
