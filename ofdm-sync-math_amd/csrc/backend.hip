@@ -414,6 +414,9 @@ __device__ void fft_lds_q(double2* buf, const double2* twq, int N, int LB) {
     }
 }
 
+#ifndef OFS_BE_RED2
+#define OFS_BE_RED2 1              // fast kernel: block sums alternate between two slot sets, one barrier each
+#endif
 #ifndef OFS_BE_ZSCAN
 #define OFS_BE_ZSCAN 1             // block sums by the zero-filled DPP ladder (0: predicated ladder, A/B)
 #endif
@@ -427,7 +430,9 @@ __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
     // total written by lane 63 itself (no readlane)
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = ofs::scan_add(v[i]);
-    lds_barrier();                                           // red's previous readers are done
+    if (!OFS_BE_RED2) lds_barrier();                         // red's previous readers are done (RED2:
+                                                             // alternating slots, the previous call's
+                                                             // barrier orders them)
     if (lane == 63)
 #pragma unroll
         for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
@@ -667,15 +672,17 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     // the phases live in the buffer between the pilot's LS and the unwrap (the pilot spectrum is in
     // registers by then), the reduction slots at its end; barriers before each window placement
     // keep the placement's writes behind the last reads of those slots
-    double* ph = reinterpret_cast<double*>(buf);                       // n_used <= 2N - 5·BW/64
-    double* red = reinterpret_cast<double*>(buf) + 2 * N - 5 * (BW / 64);
-    double* scan_tot = red + 4 * (BW / 64);
+    double* ph = reinterpret_cast<double*>(buf);                       // n_used <= 2N - 9·BW/64
+    double* red = reinterpret_cast<double*>(buf) + 2 * N - 9 * (BW / 64);
+    double* scan_tot = red + 8 * (BW / 64);
 #else
-    __shared__ double red[4 * (BW / 64)];
+    __shared__ double red[8 * (BW / 64)];
     __shared__ double scan_tot[BW / 64];
     double* ph = reinterpret_cast<double*>(twq + N / 4);   // n_used: phase / unwrap
 #endif
     constexpr bool L40 = OFS_BE_LDS40;
+    int rp = 0;                                               // block-sum slot set (RED2: alternating)
+    auto rs = [&]() -> double* { if (OFS_BE_RED2) rp ^= 1; return red + rp * 4 * (BW / 64); };
     const int U = a.n_used, LB = 31 - __clz(N);
     constexpr bool R8 = OFS_BE_R8 && SPT <= 8;           // 16 samples per thread in registers would spill
     constexpr bool PF = OFS_BE_PF && SPT <= 8 && sizeof(typename BeRaw<FMT>::T) <= 8;   // (complex128 too)
@@ -695,7 +702,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
         if (u < U) bsum[0] += (double)a.bins[u];
     }
     // the phase-slope fit's frame-invariant sums (np.mean(k), Σ kz, Σ kz² + 1e-12)
-    block_sums<1>(bsum, red);
+    block_sums<1>(bsum, rs());
     const double kmean = bsum[0] / (double)U;
     double kst[2] = {0.0, 0.0};
 #pragma unroll
@@ -707,7 +714,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
             kst[1] += kz * kz;
         }
     }
-    block_sums<2>(kst, red);
+    block_sums<2>(kst, rs());
     const double skz = kst[0], kden = kst[1] + 1e-12;
     BeWindow<FMT, SPT, NBT> pwin;
     BeCp<FMT, NBT> cpx;
@@ -739,7 +746,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
                 pp[0] += u.x * v.x + u.y * v.y;
                 pp[1] += u.y * v.x - u.x * v.y;
             }
-        block_sums<2>(pp, red);
+        block_sums<2>(pp, rs());
         cfo = -ofs_bemath::atan2_lean(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
     }
     if (a.cfo_out && be_tid() == 0) a.cfo_out[b] = cfo;
@@ -782,7 +789,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     }
     lds_barrier();
     BE_T(3)
-    const double slope = unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, red, scan_tot);
+    const double slope = unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot);
     if (be_tid() == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
         if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
@@ -819,7 +826,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
             gs[3] += r.x * r.x + r.y * r.y;
         }
     }
-    block_sums<4>(gs, red);
+    block_sums<4>(gs, rs());
     const double rr = gs[3];
     BE_T(7)
     const double2 g = cdiv(make_double2(gs[0], gs[1]), make_double2(gs[2] + 1e-12, 0.0));
@@ -835,7 +842,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
             ee[0] += er * er + ei * ei;
         }
     }
-    block_sums<1>(ee, red);
+    block_sums<1>(ee, rs());
     if (be_tid() == 0) {
         const double evm = sqrt((ee[0] / (double)U) / (rr / (double)U));
         if (a.gain_out) a.gain_out[b] = g;
