@@ -113,6 +113,11 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_HUNROLL
 #define OFS_ZC_HUNROLL 2           // helpers: rows of the gate pass unrolled (code size A/B)
 #endif
+#ifndef OFS_ZC_ISOLATE
+#define OFS_ZC_ISOLATE 0           // 1: the walker's SIMD-mates idle (A/B, r05ao: bit-identical, 0.2925 vs
+                                   // 0.2864 ms with 9 working helpers; 13 waves 0.444 - SIMD sharing is
+                                   // not what slows the walker's chain, as round 3 found by other means)
+#endif
 #ifndef OFS_ZC_QUIET
 #define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
 #endif
@@ -184,6 +189,13 @@ void zc_cfar_kernel(ZcArgs a) {
     // SIMD id so both workgroups' walkers share a SIMD, 0.38 -> 0.45 ms; an idle 8th wave as the
     // walker's SIMD partner, 0.362 -> 0.373 ms: SIMD sharing is not what slows the chain.)
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    // OFS_ZC_ISOLATE: a workgroup's waves go to the CU's SIMDs in a fixed cyclic order (wave w shares
+    // the SIMD of wave w mod 4), so waves 4, 8, ... would share the walker's SIMD and take issue
+    // slots from its dependent chain; they idle (barriers only) and the other waves are the helpers
+    constexpr int ZHE = OFS_ZC_ISOLATE ? ZH - ZH / 4 : ZH;            // helper waves doing work
+    constexpr int NJ = (ZS + ZHE - 1) / ZHE;                         // streams per helper wave
+    const bool idle_w = OFS_ZC_ISOLATE && wv > 0 && (wv & 3) == 0;
+    const int hi = OFS_ZC_ISOLATE ? wv - 1 - (wv >> 2) : wv - 1;     // helper rank (valid if !idle_w)
     const int64_t b0 = (int64_t)blockIdx.x * ZS;
     const int ns = (int)min((int64_t)ZS, a.B - b0);          // streams of this workgroup
     const int64_t n = a.n;
@@ -234,9 +246,9 @@ void zc_cfar_kernel(ZcArgs a) {
         }
     };
 
-    ZGate g[(ZS + ZH - 1) / ZH];
+    ZGate g[NJ];
 #pragma unroll
-    for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) { g[j].last_above = -1; g[j].gs = 0; g[j].pk = 0; g[j].pv = 0.0; g[j].open = 0; g[j].nev = 0; }
+    for (int j = 0; j < NJ; ++j) { g[j].last_above = -1; g[j].gs = 0; g[j].pk = 0; g[j].pv = 0.0; g[j].open = 0; g[j].nev = 0; }
     double acc = 0.0;                                         // walker lane s < ns: stream b0 + s
 
     // LDS-only barrier: the helpers' global stores are never waited for (a __syncthreads() fence
@@ -305,10 +317,9 @@ void zc_cfar_kernel(ZcArgs a) {
                 }
             }
             ZC_T(1)
-        } else if (!OFS_ZC_NOHELP && q >= 1) {
+        } else if (!OFS_ZC_NOHELP && q >= 1 && !idle_w) {
             // ---- helpers: chunk q-1 (flags, stores, gate) ----
             const int qc = q - 1;
-            constexpr int NJ = (ZS + ZH - 1) / ZH;                 // streams per helper wave
             // pass 1 (OFS_ZC_QUIET): the flags of every (row, stream) of this wave.  A chunk with no
             // above sample and no open gate (the common case: events are sparse) needs no gate
             // logic - its gate_mask rows are 0 - so the wave skips the scalar gate machine.
@@ -321,7 +332,7 @@ void zc_cfar_kernel(ZcArgs a) {
             for (int rr = 0; rr < ZR; ++rr)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const int s = (wv - 1) + ZH * j;
+                    const int s = hi + ZHE * j;
                     const int sr = s < ns ? s : 0;
 #if OFS_ZC_DIAG_NOLDS                                           // diagnostic: no helper LDS reads
                     cv[rr][j] = 1e-3 * (double)(lane + sr) + (double)qc; lv[rr][j] = cv[rr][j] * 1e30;
@@ -336,7 +347,7 @@ void zc_cfar_kernel(ZcArgs a) {
                 const bool vd = (i < n) & (i >= a.W);
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const int s = (wv - 1) + ZH * j;
+                    const int s = hi + ZHE * j;
                     const bool ab = (s < ns) & vd & (cv[rr][j] * a.scale >= lv[rr][j] * a.tv) & (cv[rr][j] >= a.minmag);
                     am[rr][j] = __ballot(ab);
                     if (am[rr][j]) quiet = false;
@@ -353,7 +364,7 @@ void zc_cfar_kernel(ZcArgs a) {
             const bool vd = inb && i >= a.W;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                const int s = (wv - 1) + ZH * j;
+                const int s = hi + ZHE * j;
                 if (s >= ns) break;
                 const double c = cv[rr][j];
                 const double ls = lv[rr][j];
@@ -430,10 +441,10 @@ void zc_cfar_kernel(ZcArgs a) {
         if (wv == 0) { ZC_T(2) } else { ZC_T(4) }
     }
     // ---- gates still open at the end: gate_end = n, gate_mask[gate_start:n] ----
-    if (wv >= 1) {
+    if (wv >= 1 && !idle_w) {
 #pragma unroll
-        for (int j = 0; j < (ZS + ZH - 1) / ZH; ++j) {
-            const int s = (wv - 1) + ZH * j;
+        for (int j = 0; j < NJ; ++j) {
+            const int s = hi + ZHE * j;
             if (s >= ns) break;
             ZGate& G = g[j];
             if (G.open) {

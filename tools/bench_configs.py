@@ -665,7 +665,7 @@ def zc_detect(dev, st, steps, warmup, state=False, seq=False):
     return dict(config=name, workload=f"zc_v2 CFAR + gate, {B} x {n} f64 |corr| (events + gate mask"
                 + (" + state arrays)" if state else ")"),
                 kernel=("zc_detect_kernel (one wave per stream, sequential recursion)" if seq else
-                        "zc_cfar_kernel (16 streams per workgroup, 1 walker + 7 helper waves: lane-per-stream recursion + closed-form gate)"),
+                        "zc_cfar_kernel (16 streams per workgroup, 1 walker + 11 helper waves: lane-per-stream recursion + closed-form gate)"),
                 samples=B * n, ms=ms, alg_bytes=B * n * (8 + 1 + (26 if state else 0)),
                 bytes_per_sample="8 in + gate 1 out" + (" + 3 x 8 + 2 x 1 state out" if state else ""))
 
