@@ -422,7 +422,7 @@ __device__ void fft_lds_q(double2* buf, const double2* twq, int N, int LB) {
 #endif
 // NV block-wide sums with one pair of barriers: DPP wave sums (inclusive scan, lane 63), then the
 // BW/64 wave totals through LDS; every thread gets the NV results.
-template <int NV>
+template <int NV, bool SYNC = false>
 __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
     const int lane = be_tid() & 63, w = be_tid() >> 6;
 #if OFS_BE_ZSCAN
@@ -430,9 +430,10 @@ __device__ __forceinline__ void block_sums(double (&v)[NV], double* red) {
     // total written by lane 63 itself (no readlane)
 #pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = ofs::scan_add(v[i]);
-    if (!OFS_BE_RED2) lds_barrier();                         // red's previous readers are done (RED2:
+    if (!OFS_BE_RED2 || SYNC) lds_barrier();                 // red's previous readers are done (RED2:
                                                              // alternating slots, the previous call's
-                                                             // barrier orders them)
+                                                             // barrier orders them; SYNC: the slots
+                                                             // overlay LDS data other waves may still read)
     if (lane == 63)
 #pragma unroll
         for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
@@ -826,7 +827,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
             gs[3] += r.x * r.x + r.y * r.y;
         }
     }
-    block_sums<4>(gs, rs());
+    block_sums<4, L40>(gs, rs());                                     // (L40: the slots overlay the data spectrum)
     const double rr = gs[3];
     BE_T(7)
     const double2 g = cdiv(make_double2(gs[0], gs[1]), make_double2(gs[2] + 1e-12, 0.0));
