@@ -571,3 +571,29 @@ def test_aa_fp32_fast_path_two_antennas(T, L):
     x = x.astype(np.complex64)
     out = sync_aa.aa_detect_streaming_batched(torch.from_numpy(x).cuda(), L=L, precision="fp32")
     check_fp32_batch(out, x, L)
+
+
+@pytest.mark.parametrize("N,U", [(1024, 600), (2048, 1200), (4096, 2400)])
+def test_receiver_backend_fast_kernel_repeatable_at_full_occupancy(N, U):
+    """The fast back-end overlays its phases and reduction slots on the sample buffer (40 KB LDS,
+    4-5 workgroups per CU): a cross-wave LDS ordering slip would show as run-to-run differences.
+    Enough frames to fill every CU several times, used bins up to the buffer's end (centered
+    subcarriers include k = -1), five calls bit for bit."""
+    rng = np.random.default_rng(N)
+    B, nb, cp = 4096, 2, min(N // 4, 512)
+    T = 2 * (N + cp) + 64
+    x = torch.from_numpy(((rng.standard_normal((B, nb, T)) + 1j * rng.standard_normal((B, nb, T))) * 100)
+                         .astype(np.complex64)).cuda()
+    k = core.centered_subcarrier_indices(U)
+    ps = rng.integers(0, 60, B)
+    ds = ps + N + cp
+    pil = np.exp(2j * np.pi * rng.random((B, k.size)))
+    dat = np.exp(2j * np.pi * rng.random(k.size))
+    runs = [core.receiver_backend_batched(x, ps, ds, pil, dat, n_fft=N, cp_len=cp, fs_hz=1e6, bins=k)
+            for _ in range(5)]
+    for r in runs[1:]:
+        for key in ("cfo", "h", "xa", "evm", "slope"):
+            a, b = runs[0][key], r[key]
+            a = torch.view_as_real(a) if a.is_complex() else a
+            b = torch.view_as_real(b) if b.is_complex() else b
+            assert torch.equal(a.view(torch.int64), b.view(torch.int64)), key
