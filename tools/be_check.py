@@ -19,11 +19,11 @@ sys.path.insert(0, os.path.join(ROOT, "ofdm-sync-math_amd"))
 from ofdm_sync_amd import _lib, core  # noqa: E402
 
 
-def run(lib, dev, st, B=16384, nb=2, N=2048, cp=512, seed=11):
+def run(lib, dev, st, B=16384, nb=2, N=2048, cp=512, seed=11, n_used=1200):
     T = 2 * (N + cp) + 64
     g = torch.Generator(device=dev).manual_seed(seed)
     x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
-    k = core.centered_subcarrier_indices(1200)
+    k = core.centered_subcarrier_indices(n_used)
     U = k.size
     ps = torch.randint(0, 60, (B,), dtype=torch.int64, device=dev, generator=g)
     ds = ps + N + cp
@@ -47,10 +47,12 @@ def main():
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
     res = []
+    N = int(os.environ.get("BE_N", "2048"))                 # BE_N=1024 / 4096: the other fast shapes
+    shape = dict(N=N, cp=min(N // 4, 512), n_used=int(N * 1200 / 2048), B=16384 * 2048 // N)
     for path in sys.argv[1:]:
         lib = ctypes.CDLL(os.path.abspath(path))
         _lib._declare(lib)
-        res.append((os.path.basename(path), run(lib, dev, st)))
+        res.append((os.path.basename(path), run(lib, dev, st, **shape)))
     base = res[0][1]
     for name, r in res[1:]:
         same = [torch.equal(a.view(torch.int64) if a.dtype == torch.float64 else torch.view_as_real(a).view(torch.int64),
