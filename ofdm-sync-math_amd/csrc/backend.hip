@@ -654,7 +654,8 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 #define OFS_BE_DEARLY 0
 #endif
 #ifndef OFS_BE_R8MAX
-#define OFS_BE_R8MAX 8             // largest SPT on the register-staged radix-8 path (16: N = 4096 too, A/B)
+#define OFS_BE_R8MAX 16            // largest SPT on the register-staged radix-8 path (N = 4096: 1.049 -> 0.898 ms
+                                   // with 215 VGPRs at its 2 workgroups per CU, r05as; 8: the LDS radix-4 path)
 #endif
 #ifndef OFS_BE_R8
 #define OFS_BE_R8 1                // 0: place_window + fft_lds_q (A/B)
@@ -688,7 +689,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     int rp = 0;                                               // block-sum slot set (RED2: alternating)
     auto rs = [&]() -> double* { if (OFS_BE_RED2) rp ^= 1; return red + rp * 4 * (BW / 64); };
     const int U = a.n_used, LB = 31 - __clz(N);
-    constexpr bool R8 = OFS_BE_R8 && SPT <= OFS_BE_R8MAX;  // (round 3: 16 samples per thread spilled)
+    constexpr bool R8 = OFS_BE_R8 && SPT <= OFS_BE_R8MAX;  // (round 3, with ocml math: 16 samples per thread spilled)
     constexpr bool PF = OFS_BE_PF && SPT <= 8 && sizeof(typename BeRaw<FMT>::T) <= 8;   // (complex128 too)
     for (int j = threadIdx.x; j < N / 4; j += BW) {
         double sn, cs;
