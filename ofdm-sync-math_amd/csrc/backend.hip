@@ -653,6 +653,9 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 #ifndef OFS_BE_DEARLY
 #define OFS_BE_DEARLY 0
 #endif
+#ifndef OFS_BE_CPFIRST
+#define OFS_BE_CPFIRST 0           // 1: CP loads issued before the pilot window's (A/B, r05au: 0.712 vs 0.709 ms
+#endif                             // at N 2048, 0.831 vs 0.818 at 1024, 0.895 vs 0.898 at 4096 - off)
 #ifndef OFS_BE_R8MAX
 #define OFS_BE_R8MAX 16            // largest SPT on the register-staged radix-8 path (N = 4096: 1.049 -> 0.898 ms
                                    // with 215 VGPRs at its 2 workgroups per CU, r05as; 8: the LDS radix-4 path)
@@ -734,9 +737,14 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     lds_barrier();
     const int64_t ps = a.pilot_start[b], ds = a.data_start[b];
-    if (!PF) {
-        pwin.issue(a, b, ps + a.cp);
-        cpx.issue(a, b, ps);
+    if (!PF) {                        // (CPFIRST: the CFO would wait for the CP samples alone - vmcnt
+        if (OFS_BE_CPFIRST) {         // counts in order - with the pilot window's loads still in flight)
+            cpx.issue(a, b, ps);
+            pwin.issue(a, b, ps + a.cp);
+        } else {
+            pwin.issue(a, b, ps + a.cp);
+            cpx.issue(a, b, ps);
+        }
     }
     double cfo;
     if (a.cfo_in) {
