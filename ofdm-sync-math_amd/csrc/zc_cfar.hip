@@ -121,6 +121,20 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_QUIET
 #define OFS_ZC_QUIET 1             // 0: gate machine on every row (A/B)
 #endif
+// state / mask stores of the helpers: non-temporal (streamed past the caches; nothing here reads
+// them back).  r05av, bit-identical: state arrays 0.63 -> 0.56 ms, events + mask unchanged (0.286)
+#ifndef OFS_ZC_NT
+#define OFS_ZC_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void zc_st(T* p, T v) {
+#if OFS_ZC_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // walker: the exact left-to-right recursion of RunningSum.step over one full chunk of this lane's
 // stream; LDS reads a batch ahead of the dependent adds (the chain is 2 v_add_f64 per sample; an
 // LDS round trip per sample would set the pace instead).  OZ: c[i-W] is 0 (window not yet full).
@@ -374,12 +388,12 @@ void zc_cfar_kernel(ZcArgs a) {
                 const int64_t o = (b0 + s) * n + i;
                 if (quiet) {
                     if (inb && !OFS_ZC_DIAG_NOST) {
-                        if (a.local_sum) a.local_sum[o] = ls;
-                        if (a.corr_scaled) a.corr_scaled[o] = cs;
-                        if (a.thresh_scaled) a.thresh_scaled[o] = th;
-                        if (a.above) a.above[o] = 0;
-                        if (a.valid) a.valid[o] = (uint8_t)vd;
-                        if (a.gate_mask) a.gate_mask[o] = 0;
+                        if (a.local_sum) zc_st(&a.local_sum[o], ls);
+                        if (a.corr_scaled) zc_st(&a.corr_scaled[o], cs);
+                        if (a.thresh_scaled) zc_st(&a.thresh_scaled[o], th);
+                        if (a.above) zc_st(&a.above[o], (uint8_t)0);
+                        if (a.valid) zc_st(&a.valid[o], (uint8_t)vd);
+                        if (a.gate_mask) zc_st(&a.gate_mask[o], (uint8_t)0);
                     }
                     continue;
                 }
@@ -426,12 +440,12 @@ void zc_cfar_kernel(ZcArgs a) {
                 }
                 if (abm) G.last_above = base + 63 - __builtin_clzll(abm);
                 if (inb) {
-                    if (a.local_sum) a.local_sum[o] = ls;
-                    if (a.corr_scaled) a.corr_scaled[o] = cs;
-                    if (a.thresh_scaled) a.thresh_scaled[o] = th;
-                    if (a.above) a.above[o] = (uint8_t)ab;
-                    if (a.valid) a.valid[o] = (uint8_t)vd;
-                    if (a.gate_mask) a.gate_mask[o] = (uint8_t)mk;
+                    if (a.local_sum) zc_st(&a.local_sum[o], ls);
+                    if (a.corr_scaled) zc_st(&a.corr_scaled[o], cs);
+                    if (a.thresh_scaled) zc_st(&a.thresh_scaled[o], th);
+                    if (a.above) zc_st(&a.above[o], (uint8_t)ab);
+                    if (a.valid) zc_st(&a.valid[o], (uint8_t)vd);
+                    if (a.gate_mask) zc_st(&a.gate_mask[o], (uint8_t)mk);
                 }
             }
             }
