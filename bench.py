@@ -336,6 +336,9 @@ def main(argv=None):
         dist.barrier()
     ms_max = shard.max_over_ranks(ms, dist, dev)
     ms_per_step = ms_max / a.steps
+    census = shard.rank_census(dist, dev, ms, (lo, lo + B))     # ranks the collective saw, per-rank device + ms
+    if census["ranks_seen"] != world or not census["distinct_devices"]:
+        raise SystemExit(f"bench.py: rank census disagrees with WORLD_SIZE={world}: {census}")
 
     total_samples = B_glob * T * a.steps
     value = total_samples / (ms_max / 1e3) / 1e6
@@ -359,9 +362,13 @@ def main(argv=None):
                    "global_batch": B_glob, "seq_len": T, "L": L,
                    "parallelism": f"stream-shard x{world} (no collectives)",
                    "placement": a.placement if a.selftest_cpu else f"{a.placement} -> {det.placement}"},
+        "ranks_seen": census["ranks_seen"],
+        "rank_devices": [r["device"] for r in census["ranks"]],
+        "rank_ms": [r["ms"] for r in census["ranks"]],
+        "rank_shards": [r["shard"] for r in census["ranks"]],
     }
     if a.selftest_cpu:
-        out.update(selftest=True, rank_ms=ms, shard=[lo, lo + B])
+        out.update(selftest=True, shard=[lo, lo + B])
         if rank == 0:
             print(json.dumps(out), flush=True)
         if dist:

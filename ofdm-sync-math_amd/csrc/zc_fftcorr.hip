@@ -603,6 +603,13 @@ __device__ __forceinline__ double mp_sqrt(double x) {
     if (x < 0x1p-1000) return sqrt(x);
     return x * mp_rsqrt(x);
 }
+// |c| (np.abs): mp_sqrt of |c|^2, or hypot where |c|^2 overflows (|c| > ~1.3e154: rsqrt(inf) = 0 would
+// give inf·0 = NaN; numpy's hypot stays finite) or is NaN
+__device__ __forceinline__ double mp_cabs(double2 c) {
+    const double x = fma(c.x, c.x, c.y * c.y);
+    if (!(x <= 0x1.fffffffffffffp+1023)) return hypot(c.x, c.y);
+    return mp_sqrt(x);
+}
 
 // a block's samples t + 512m (zero outside the stream)
 template <int FMT>
@@ -810,7 +817,7 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             const int64_t oi = row * a.nout + n0 + s;               // one branch: row = stream
             if (a.mode == OFS_ZC_RAW || a.mode == OFS_ZC_SUM) {
                 if (a.out && st_ok) a.out[oi] = c;
-                if (a.mag && st_ok) a.mag[oi] = mp_sqrt(fma(c.x, c.x, c.y * c.y));
+                if (a.mag && st_ok) a.mag[oi] = mp_cabs(c);
                 continue;
             }
 #if OFS_MP_AB & 4
@@ -826,10 +833,10 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             const double2 r = make_double2(c.x * inv, c.y * inv);
 #if OFS_MP_NTST                     // tuning builds: non-temporal output stores
             if (a.out && st_ok) { __builtin_nontemporal_store(r.x, &a.out[oi].x); __builtin_nontemporal_store(r.y, &a.out[oi].y); }
-            if (a.mag && st_ok) __builtin_nontemporal_store(mp_sqrt(fma(r.x, r.x, r.y * r.y)), &a.mag[oi]);
+            if (a.mag && st_ok) __builtin_nontemporal_store(mp_cabs(r), &a.mag[oi]);
 #else
             if (a.out && st_ok) a.out[oi] = r;
-            if (a.mag && st_ok) a.mag[oi] = mp_sqrt(fma(r.x, r.x, r.y * r.y));
+            if (a.mag && st_ok) a.mag[oi] = mp_cabs(r);
 #endif
         }
         MP_T_MARK(7);

@@ -127,39 +127,42 @@ __global__ __launch_bounds__(ZWG) void zc_gather_kernel(GatherArgs a) {
 }
 
 // rows plans: metric[b][off] for every offset of the execution's streams from the compact spectrum of
-// windows w = (b·n_br + br)·T + off.  One wave per (stream, offset), lane k = template bin k.
+// windows w = (b·n_br + br)·T + off.  One wave per (stream, offset), lane k = template bin k; the
+// streams stride over gridDim.y (<= 65535, the launch limit), so any rows-per-execution fits.
 template <class R>
 __global__ __launch_bounds__(ZWG) void zc_gather_rows_kernel(GatherArgs a, int64_t T) {
     const int lane = threadIdx.x & 63;
-    const int64_t off = (int64_t)blockIdx.x * (ZWG / 64) + (threadIdx.x >> 6), b = blockIdx.y;
+    const int64_t off = (int64_t)blockIdx.x * (ZWG / 64) + (threadIdx.x >> 6);
     if (off >= a.n_off) return;
-    double cr = 0.0, ci = 0.0, en = 0.0;
-    if (lane < a.n_bins) {
-        const double tr = a.t_re[lane], ti = a.t_im[lane];
-        for (int br = 0; br < a.n_br; ++br) {
-            const int64_t i = ((b * a.n_br + br) * T + off) * a.n_bins + lane;
-            double xr, xi;
-            if constexpr (sizeof(R) == 4) {
-                const float2 v = reinterpret_cast<const float2*>(a.spec)[i];
-                xr = v.x; xi = v.y;
-            } else {
-                const double2 v = reinterpret_cast<const double2*>(a.spec)[i];
-                xr = v.x; xi = v.y;
+    for (int64_t b = blockIdx.y; b < a.B; b += gridDim.y) {
+        double cr = 0.0, ci = 0.0, en = 0.0;
+        if (lane < a.n_bins) {
+            const double tr = a.t_re[lane], ti = a.t_im[lane];
+            for (int br = 0; br < a.n_br; ++br) {
+                const int64_t i = ((b * a.n_br + br) * T + off) * a.n_bins + lane;
+                double xr, xi;
+                if constexpr (sizeof(R) == 4) {
+                    const float2 v = reinterpret_cast<const float2*>(a.spec)[i];
+                    xr = v.x; xi = v.y;
+                } else {
+                    const double2 v = reinterpret_cast<const double2*>(a.spec)[i];
+                    xr = v.x; xi = v.y;
+                }
+                cr += tr * xr + ti * xi;                     // conj(t) * x   (zc_freq.py:88-95)
+                ci += tr * xi - ti * xr;
+                en += xr * xr + xi * xi;
             }
-            cr += tr * xr + ti * xi;                     // conj(t) * x   (zc_freq.py:88-95)
-            ci += tr * xi - ti * xr;
-            en += xr * xr + xi * xi;
         }
-    }
-    for (int m = 32; m >= 1; m >>= 1) {
-        cr += __shfl_xor(cr, m);
-        ci += __shfl_xor(ci, m);
-        en += __shfl_xor(en, m);
-    }
-    if (lane == 0) {
-        const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
-        if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[(a.b0 + b) * a.n_off + off] = (float)v;
-        else reinterpret_cast<double*>(a.metric)[(a.b0 + b) * a.n_off + off] = v;
+        for (int m = 32; m >= 1; m >>= 1) {
+            cr += __shfl_xor(cr, m);
+            ci += __shfl_xor(ci, m);
+            en += __shfl_xor(en, m);
+        }
+        if (lane == 0) {
+            const double v = (cr * cr + ci * ci) / fmax(a.e_t * en, 1e-12);
+            if constexpr (sizeof(R) == 4) reinterpret_cast<float*>(a.metric)[(a.b0 + b) * a.n_off + off] = (float)v;
+            else reinterpret_cast<double*>(a.metric)[(a.b0 + b) * a.n_off + off] = v;
+        }
     }
 }
 
@@ -458,7 +461,7 @@ int32_t ofs_zc_freq_metric_fft(void* plan, int32_t in_fmt, const void* x, int64_
             if (s != rocfft_status_success) break;
             g.b0 = r0 / n_br;
             g.B = nr / n_br;
-            const dim3 gr((unsigned)((n_off + ZWG / 64 - 1) / (ZWG / 64)), (unsigned)g.B);
+            const dim3 gr((unsigned)((n_off + ZWG / 64 - 1) / (ZWG / 64)), (unsigned)(g.B < 65535 ? g.B : 65535));
             if (p->precision == OFS_FP32) hipLaunchKernelGGL(zc_gather_rows_kernel<float>, gr, dim3(ZWG), 0, st, g, T);
             else hipLaunchKernelGGL(zc_gather_rows_kernel<double>, gr, dim3(ZWG), 0, st, g, T);
             if (hipGetLastError() != hipSuccess) rc = OFS_EHIP;

@@ -60,6 +60,41 @@ def max_over_ranks(x: float, dist, device) -> float:
     return float(t.item())
 
 
+def rank_census(dist, device, rank_ms: float, shard: tuple[int, int]) -> dict:
+    """Self-verification of a multi-rank run (control plane only): an all-reduce of ones over the
+    ranks (how many ranks the collective actually saw) and an all-gather of each rank's
+    (rank, local rank, device ordinal, PCI domain/bus/device, timed ms, shard bounds).  On a GPU
+    the PCI address is the HIP device's (torch.cuda.get_device_properties); on CPU (gloo
+    self-test) the "device" is the rank's process, labelled cpu:<local rank>.  Returns
+    {"ranks_seen": n, "ranks": [{...} per rank in rank order], "distinct_devices": bool}."""
+    info = rank_info()
+    on_gpu = device is not None and device.type == "cuda"
+    if on_gpu:
+        p = torch.cuda.get_device_properties(device)
+        ident = [float(device.index), float(getattr(p, "pci_domain_id", -1)), float(getattr(p, "pci_bus_id", -1)),
+                 float(getattr(p, "pci_device_id", -1))]
+    else:
+        ident = [float(info.local_rank), -1.0, -1.0, -1.0]
+    row = torch.tensor([float(info.rank), float(info.local_rank), *ident, float(rank_ms), float(shard[0]),
+                        float(shard[1])], dtype=torch.float64, device=device)
+    one = torch.ones(1, dtype=torch.float64, device=device)
+    if dist is not None:
+        dist.all_reduce(one, op=dist.ReduceOp.SUM)
+        rows = [torch.zeros_like(row) for _ in range(dist.get_world_size())]
+        dist.all_gather(rows, row)
+    else:
+        rows = [row]
+    ranks = []
+    for r in rows:
+        v = r.cpu().tolist()
+        dev = (f"cuda:{int(v[2])} pci {int(v[3]):04x}:{int(v[4]):02x}:{int(v[5]):02x}" if on_gpu
+               else f"cpu:{int(v[2])}")
+        ranks.append(dict(rank=int(v[0]), local_rank=int(v[1]), device=dev, ms=round(v[6], 5),
+                          shard=[int(v[7]), int(v[8])]))
+    return dict(ranks_seen=int(round(float(one.item()))), ranks=ranks,
+                distinct_devices=len({r["device"] for r in ranks}) == len(ranks))
+
+
 def gather_counts(counts: torch.Tensor, dist) -> torch.Tensor:
     """Concatenate per-rank 1-D result tensors in rank order (validation only)."""
     if dist is None:

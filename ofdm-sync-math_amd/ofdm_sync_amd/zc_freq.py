@@ -158,13 +158,31 @@ def _plan(precision: int, N: int, n_windows: int, T: int, prune_bins: int = 0, c
 
 
 ROWS_SPECTRUM_BYTES = 256 << 20     # compact spectrum of one rows-plan execution (rows_per_exec sizing)
-ROWS_MIN_OFFSETS = 8                # layout "auto": the rows plan from this many offsets per stream on
+ROWS_MIN_OFFSETS = 8                # layout "auto": the rows plan from this many offsets per stream on ...
+ROWS_MAX_RATIO = 4                  # ... and only while T <= ROWS_MAX_RATIO x offsets: a rows plan transforms
+                                    # about T windows per row where the offsets plan transforms n_off, so
+                                    # T / n_off is its extra FFT work (r05c, T 4242 / 1683 offsets = 2.5x:
+                                    # rows 20.1 vs offsets 49.2 ms - the launches it saves paid for it)
 
 
 def rows_per_exec(n_rows: int, n_br: int, T: int, n_bins: int, esz: int) -> int:
     """Rows per rows-plan execution: a compact spectrum of about ROWS_SPECTRUM_BYTES, whole streams."""
     per = max(n_br, (ROWS_SPECTRUM_BYTES // max(1, T * n_bins * esz)) // n_br * n_br)
-    return min(per, n_rows)
+    return min(per, n_rows)                  # (the gather strides its streams over gridDim.y: no 65535 cap)
+
+
+def pick_rows_layout(layout: str, prunable: bool, chunk, T: int, n_off: int) -> bool:
+    """True when compute_frequency_metric_rocfft_batched takes the rows plan: layout "rows", or "auto"
+    with a prunable template, no ``chunk`` (it counts windows of the offsets layout), at least
+    ROWS_MIN_OFFSETS offsets and T <= ROWS_MAX_RATIO x n_off."""
+    if layout not in ("auto", "offsets", "rows"):
+        raise ValueError("layout must be 'auto', 'offsets' or 'rows'")
+    if layout == "rows" and not prunable:
+        raise ValueError("layout='rows' needs a prunable template (N a power of two <= 4096, distinct bins)")
+    if layout == "rows" and chunk:
+        raise ValueError("layout='rows' takes rows_per_execution; chunk counts windows of the offsets layout")
+    return layout == "rows" or (layout == "auto" and prunable and chunk is None and n_off >= ROWS_MIN_OFFSETS
+                                and T <= ROWS_MAX_RATIO * n_off)
 
 
 def default_chunk(n_windows: int, n_br: int, N: int, esz: int) -> int:
@@ -180,7 +198,8 @@ CHUNK_BYTES = 64 << 20
 def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=None, template_energy=None,
                                             N: int | None = None, cp: int | None = None, *,
                                             return_peak: bool = False, pruned: bool = False,
-                                            chunk: int | None = None, layout: str = "auto"):
+                                            chunk: int | None = None, layout: str = "auto",
+                                            rows_per_execution: int | None = None):
     """compute_frequency_metric (zc_freq.py:62-99) over x[B, n_branch, T] through rocFFT: one
     batched FFT of every stream/branch window per offset, then the 62-bin gather and metric.
     complex64 input -> f32 metric, complex128 -> f64.  With ``return_peak`` also returns the
@@ -196,8 +215,12 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     ``layout``: "offsets" - one rocFFT execution (+ gather) per offset, as above; "rows" - one execution
     per group of rows covering every offset of them (windows one sample apart, always pruned:
     ofs_zc_fft_plan_create_rows), 2 launches per row group instead of 2 per offset - the form for the
-    reference's own sliding shape (thousands of offsets per stream); "auto": "rows" from
-    ROWS_MIN_OFFSETS offsets per stream on when the template is prunable, else "offsets"."""
+    reference's own sliding shape (thousands of offsets per stream); "auto": "rows" when the template is
+    prunable, ``chunk`` is not given, there are at least ROWS_MIN_OFFSETS offsets per stream and
+    T <= ROWS_MAX_RATIO x offsets (the rows plan's extra FFT work, T / offsets, stays small), else
+    "offsets".  ``rows_per_execution``: rows (stream x branch) per rows-plan execution (None or 0:
+    ``rows_per_exec`` sizes a ~256 MiB compact spectrum); ``chunk`` is the offsets layout's windows per
+    execution and is refused with layout="rows"."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -221,11 +244,7 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
                     torch.empty((0,), dtype=torch.float64, device=dev))
         return out
     prunable = N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
-    if layout not in ("auto", "offsets", "rows"):
-        raise ValueError("layout must be 'auto', 'offsets' or 'rows'")
-    if layout == "rows" and not prunable:
-        raise ValueError("layout='rows' needs a prunable template (N a power of two <= 4096, distinct bins)")
-    rows = layout == "rows" or (layout == "auto" and prunable and noff >= ROWS_MIN_OFFSETS)
+    rows = pick_rows_layout(layout, prunable, chunk, batch.T, noff)
     pruned = (bool(pruned) or rows) and prunable
     nw = batch.B * batch.nb
     out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
@@ -233,9 +252,9 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     pv = torch.empty((batch.B,), dtype=torch.float64, device=dev) if return_peak else None
     if rows:
         esz = 8 if prec == _lib.FP32 else 16
-        rpe = int(chunk) if chunk else rows_per_exec(nw, batch.nb, batch.T, int(idx.size), esz)
+        rpe = int(rows_per_execution) if rows_per_execution else rows_per_exec(nw, batch.nb, batch.T, int(idx.size), esz)
         if rpe % batch.nb:
-            raise ValueError("chunk (rows per execution) must be a multiple of the branch count")
+            raise ValueError("rows_per_execution must be a multiple of the branch count")
         plan = _plan(prec, N, nw, batch.T, int(idx.size), rpe, rows_cp=cp)
         spec = torch.empty((plan.chunk, int(idx.size)), dtype=batch.data.dtype, device=dev)
         work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None

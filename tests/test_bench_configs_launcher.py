@@ -33,7 +33,10 @@ def test_gpus2_strong_scaling_cfg4_cfg5():
         assert r["samples"] == total * 4096                       # both ranks' shards summed
         assert r["alg_bytes"] == total * 4096 * 8
         # rank 1 sleeps 4 ms per step, rank 0 2 ms: the reported time is rank 1's (MAX over ranks)
-        assert r["ms"] >= 0.95 * 4.0 and r["rank_ms"] < r["ms"]
+        assert r["ms"] >= 0.95 * 4.0 and r["rank_ms"][0] < r["ms"]
+        assert r["ms"] == pytest.approx(max(r["rank_ms"]), rel=1e-4)
+        assert r["ranks_seen"] == 2 and r["rank_devices"] == ["cpu:0", "cpu:1"]
+        assert r["rank_shards"] == [[0, (total + 1) // 2], [(total + 1) // 2, total]]
         assert r["value"] == pytest.approx(total * 4096 / (r["ms"] / 1e3) / 1e6, rel=1e-3)
         assert r["hbm_frac"] == pytest.approx(r["achieved_GBs"] / (8000.0 * 2), abs=1e-4)   # vs 2 GPUs of HBM
 
@@ -43,6 +46,7 @@ def test_gpus2_per_rank_config_and_overrides():
     rs = _run("--gpus", "2", "--configs", "cfg2b@B=100", "--steps", "1", "--warmup", "0")
     assert len(rs) == 1 and rs[0]["scaling"] == "per-rank" and rs[0]["n_gpus"] == 2
     assert rs[0]["samples"] == 100 * 4096                         # keyword override reached the config
+    assert rs[0]["ranks_seen"] == 2 and len(set(rs[0]["rank_devices"])) == 2
 
 
 def test_world_size_mismatch_fails_loudly():

@@ -209,7 +209,7 @@ def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe):
     idx, t, e = O.zc_template()
     xd = torch.from_numpy(x).cuda()
     r, pr, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
-                                                               layout="rows", chunk=rpe)
+                                                               layout="rows", rows_per_execution=rpe)
     o, po, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
                                                                layout="offsets", pruned=True)
     a, b_ = r.cpu().numpy(), o.cpu().numpy()

@@ -763,10 +763,18 @@ def main(argv=None):
             if _DIST is not None:
                 _DIST.all_reduce(tot)
             r["samples"], r["alg_bytes"] = int(tot[0].item()), int(tot[1].item())
+            census = shard.rank_census(_DIST, dev, ms_rank, (lo, hi))
             r.update(scaling="strong", global_batch=getattr(a, SHARDED[name][0]), n_gpus=info.world,
-                     shard=[lo, hi], rank_ms=round(ms_rank, 4))
+                     shard=[lo, hi])
         else:
+            census = shard.rank_census(_DIST, dev, ms_rank, (0, 0))
             r.update(scaling="per-rank", n_gpus=info.world)
+        if census["ranks_seen"] != info.world or not census["distinct_devices"]:
+            raise SystemExit(f"bench_configs.py: rank census disagrees with WORLD_SIZE={info.world}: {census}")
+        r.update(ranks_seen=census["ranks_seen"], rank_devices=[c["device"] for c in census["ranks"]],
+                 rank_ms=[c["ms"] for c in census["ranks"]])
+        if name in SHARDED:
+            r["rank_shards"] = [c["shard"] for c in census["ranks"]]
         r["ms"] = ms
         if _LAST_HOST_MS is not None:
             r["host_ms_per_step"] = round(_LAST_HOST_MS, 4)
