@@ -41,6 +41,7 @@ constexpr int FAST_WG = OFS_FAST_WG;   // one wave = one stream per workgroup (p
 #define OFS_FAST_BOUNDS __launch_bounds__(FAST_WG)
 #endif
 constexpr int TMAX = 1024;        // stream length handled by the fast path
+constexpr int FAST_CAP_LDS = 160 * 1024 / 10;   // occupancy cap of the storing kernel: 10 workgroups per CU (launch)
 
 // cache policy knobs (tuning builds): non-temporal output stores, LDS-DMA aux bits
 #ifndef OFS_STORE_NT
@@ -49,7 +50,8 @@ constexpr int TMAX = 1024;        // stream length handled by the fast path
 #ifndef OFS_DMA_AUX
 #define OFS_DMA_AUX 0
 #endif
-// stream staging: 0 = LDS-DMA (global_load_lds_dwordx4), 1 = registers
+// stream staging: 0 = LDS-DMA (global_load_lds_dwordx4), 1 = registers, 2 = registers with the loads
+// pinned as inline asm + per-row vmcnt waits (tuning builds; r06b below)
 #ifndef OFS_FAST_STAGE
 #define OFS_FAST_STAGE 1
 #endif
@@ -87,6 +89,11 @@ __device__ __forceinline__ void st_out(float2* p, float2 v) {
 // of this read/write pattern).  Round 2, with the DMA as inline asm and per-row vmcnt waits (the
 // builtin made the compiler wait for the whole stream before the first row) and 107 instead of
 // 139 VGPRs (4 waves/SIMD): still 3 % slower (0.315 vs 0.305 ms, profiles/r02av_staging_ab.jsonl).
+// Round 6, the loads pinned (OFS_FAST_STAGE=2: inline-asm global_load_dwordx4, per-row vmcnt) so a
+// tight register budget cannot defer them: 105 VGPRs at 4 waves/SIMD, no spills, bit-identical - and
+// more waves are SLOWER, not faster (paired, 9 rotated rounds, profiles/r06b_headline_pinned_loads_
+// waves_ab.jsonl): 3 waves 0.3067 ms (plain) / 0.3082 (pinned), 4 waves 0.3150 (pinned) / 0.3137
+// (plain), 5 waves 0.3283 (pinned).  The kernel is not latency-starved at 3 waves/SIMD.
 // scan-free gate flags in the P/R/M-storing instantiation too (tuning builds: -DOFS_FAST_FF=1)
 #ifndef OFS_FAST_FF
 #define OFS_FAST_FF 0
@@ -140,6 +147,39 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     auto row_wait = [&](int k) {
         if (all_out) ofs::vmcnt_wait((RW - 1 - k) * NA * V4 + k * SPR);
         else ofs::vmcnt_wait((RW - 1 - k) * NA * V4);
+    };
+#elif OFS_FAST_STAGE == 2
+    // register staging with the loads PINNED at the top: each load is an inline-asm
+    // global_load_dwordx4 (the compiler cannot sink it under a tight register budget, which is
+    // what the plain loads did at 4 waves/SIMD), each row's first use waits with its own
+    // s_waitcnt vmcnt(n) - n = the younger operations still allowed in flight, vmcnt counting
+    // in order: the loads of later rows, plus, for a full stream (T = TMAX, every row's stores
+    // issued by every lane) with P, R and M all stored, the SPR stores of each earlier row.  Any
+    // other shape counts the loads alone (the stores then only lengthen the wait).  An empty asm
+    // that rewrites the row's registers right after the wait keeps their uses behind it.
+    constexpr int SPR = V4 + ((E % 4 != 0) ? 2 * V4 : 2 * (V4 / 2));   // P + R + M stores per row
+    nf4 xreg[NA][RW][V4];
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            const float2* xs = reinterpret_cast<const float2*>(a.x) + (b * NA + t) * a.T;
+#pragma unroll
+            for (int j = 0; j < V4; ++j) {
+                int n = RL * k + E * lane + 2 * j;
+                n = n < T ? n : T - 2;                          // in-bounds; zeroed on read
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(xreg[t][k][j]) : "v"(xs + n) : "memory");
+            }
+        }
+    const bool count_st = !DO && a.P && a.R && a.M && T == TMAX;
+    auto ldrow = [&](int t, int k, int j) { const nf4 v = xreg[t][k][j]; return make_float4(v.x, v.y, v.z, v.w); };
+    auto row_wait = [&](int k) {
+        if (count_st) ofs::vmcnt_wait((RW - 1 - k) * NA * V4 + k * SPR);
+        else ofs::vmcnt_wait((RW - 1 - k) * NA * V4);
+#pragma unroll
+        for (int t = 0; t < NA; ++t)
+#pragma unroll
+            for (int j = 0; j < V4; ++j) asm volatile("" : "+v"(xreg[t][k][j]));
     };
 #else
     // register staging: every row of the lane's samples is loaded up front (RW * V4 float4), each
@@ -608,10 +648,18 @@ int launch(const AaFastArgs& a, hipStream_t st) {
     const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
     const bool s32 = scan32(det_only);
     const dim3 grid((unsigned)((a.B + FAST_WG / 64 - 1) / (FAST_WG / 64))), blk(FAST_WG);
-    if (det_only && s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, true>), grid, blk, 0, st, a);
-    else if (det_only) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, false>), grid, blk, 0, st, a);
-    else if (s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, true>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, false>), grid, blk, 0, st, a);
+    // Occupancy cap: the P/R/M-storing one-antenna kernel runs 10 workgroups (waves) per CU instead
+    // of the 12 its 139 VGPRs allow, through 16 KiB of unused dynamic LDS per workgroup (160 KiB per
+    // CU / 10).  Paired, 11 rotated rounds on the headline (profiles/r06d_headline_occupancy_sweep.json):
+    // 12 per CU 0.2980 ms, 11 0.2920, 10 0.2908, 9 0.2948, 8 0.2954 - fewer streams in flight per CU
+    // beat more (so do 3 vs 4 vs 5 waves/SIMD, r06b).  variant FAST_LDS = bytes per workgroup
+    // overrides (1: no cap, A/B).
+    const int64_t pad = ofs::variant_or(ofs::V_FAST_LDS, (!det_only && NA == 1) ? FAST_CAP_LDS : 0);
+    const size_t shm = pad > 0 && pad <= 65536 ? (size_t)pad : 0;
+    if (det_only && s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, true>), grid, blk, shm, st, a);
+    else if (det_only) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, true, false>), grid, blk, shm, st, a);
+    else if (s32) hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, true>), grid, blk, shm, st, a);
+    else hipLaunchKernelGGL((aa_fast_kernel<E, MR, NA, false, false>), grid, blk, shm, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 

@@ -13,7 +13,7 @@ namespace ofs {
 enum Variant : int {
     V_EXACT, V_FAST_E, V_FAST_E_DO, V_FAST_SCAN, V_FAST_SCAN_DO, V_RTL_WPB, V_PARK_DIRECT, V_ZW64,
     V_ZW64_GRID, V_ZS, V_ZF_ITEMS, V_ZS_PAIR, V_ZS_DEFER, V_ZS_BPL, V_ZS_C, V_ZS_GBLK, V_MC_FUSED,
-    V_MC_FUSE_X, V_ZC_SEQ, V_ZC_NODMA, V_BE_FAST, V_MC_PERS, V_COUNT
+    V_MC_FUSE_X, V_ZC_SEQ, V_ZC_NODMA, V_BE_FAST, V_MC_PERS, V_FAST_LDS, V_COUNT
 };
 int64_t variant(Variant v);                                     // INT64_MIN when unset
 inline bool variant_is(Variant v, int64_t value) { return variant(v) == value; }
