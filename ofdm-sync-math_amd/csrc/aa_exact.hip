@@ -869,11 +869,11 @@ bool exact_enabled() {                  // variant EXACT=0 forces the general en
 template <int E, int MR, int NA>
 int aa_launch(int fmt, const AaFastArgs& a, hipStream_t st) {
     if (fmt == OFS_C128)
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
     else if (fmt == OFS_CP12)
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_CP12, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CP12, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
     else
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), 0, st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 template <int E, int MR>
@@ -902,7 +902,7 @@ int rtl_launch_k(const RtlExactArgs& a, hipStream_t st) {
     const int64_t wv = ofs::variant(ofs::V_RTL_WPB);        // tuning: 1, 2 or 4
     if (wv == 1 || wv == 2) wpb = (int)wv;
     while (wpb > 1 && per_wave * wpb > 64 * 1024) wpb >>= 1;
-    const size_t lds = per_wave * wpb;
+    const size_t lds = per_wave * wpb + ofs::occ_lds();
     auto k = rtl_exact_kernel<E, MW, CPNA, NBM>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -616,10 +616,21 @@ template <int E, int MR, int NA>
 int launch_stream(const AaFastArgs& a, hipStream_t st) {
     const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
     const int64_t grid = (a.B + STREAM_WG / 64 - 1) / (STREAM_WG / 64);
+    // occupancy cap of the two-antenna storing kernel: 24 KiB of LDS per workgroup in all (unused
+    // dynamic LDS on top of its 8 KiB lag ring at L 512) = 6 workgroups per CU.  Paired on the
+    // reference's detector shape (16384 x 2 x 5315, L 512; 3 rounds, profiles/r06g_occupancy_sweeps.txt):
+    // lag ring alone 0.6005 ms, + 8 KiB 0.5843, + 12 KiB 0.5783, + 16 KiB 0.5737, + 20 KiB 0.6044
+    // (~27 KiB per workgroup rounds up past 160 KiB / 6: 5 per CU); one antenna at T = 4096 is faster
+    // uncapped (1.186 vs 1.228 ms).  variant OCC_LDS (bytes added) overrides.
+    using S = AaStream<E, MR, NA, false>;
+    constexpr size_t lag_lds = (size_t)(STREAM_WG / 64) * (S::LDSLAG ? MR : 1) * NA * S::V4 * 64 * 16;
+    constexpr size_t cap_total = 24 * 1024;
+    const size_t dflt = (!det_only && NA == 2 && cap_total > lag_lds) ? cap_total - lag_lds : 0;
+    const size_t shm = ofs::variant(ofs::V_OCC_LDS) == INT64_MIN ? dflt : ofs::occ_lds();
     if (det_only)
-        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(STREAM_WG), 0, st, a);
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(STREAM_WG), shm, st, a);
     else
-        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(STREAM_WG), 0, st, a);
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(STREAM_WG), shm, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 

@@ -816,7 +816,7 @@ int32_t ofs_version(void) { return 100; }
 static const char* const kVariantNames[ofs::V_COUNT] = {
     "EXACT", "FAST_E", "FAST_E_DO", "FAST_SCAN", "FAST_SCAN_DO", "RTL_WPB", "PARK_DIRECT", "ZW64",
     "ZW64_GRID", "ZS", "ZF_ITEMS", "ZS_PAIR", "ZS_DEFER", "ZS_BPL", "ZS_C", "ZS_GBLK", "MC_FUSED",
-    "MC_FUSE_X", "ZC_SEQ", "ZC_NODMA", "BE_FAST", "MC_PERS", "FAST_LDS"};
+    "MC_FUSE_X", "ZC_SEQ", "ZC_NODMA", "BE_FAST", "MC_PERS", "FAST_LDS", "OCC_LDS"};
 // Per calling thread: a variant one thread sets steers only the calls that thread makes, so
 // concurrent callers (another thread's production calls) never see a test's forced kernel.
 struct VariantTable {

@@ -13,13 +13,16 @@ namespace ofs {
 enum Variant : int {
     V_EXACT, V_FAST_E, V_FAST_E_DO, V_FAST_SCAN, V_FAST_SCAN_DO, V_RTL_WPB, V_PARK_DIRECT, V_ZW64,
     V_ZW64_GRID, V_ZS, V_ZF_ITEMS, V_ZS_PAIR, V_ZS_DEFER, V_ZS_BPL, V_ZS_C, V_ZS_GBLK, V_MC_FUSED,
-    V_MC_FUSE_X, V_ZC_SEQ, V_ZC_NODMA, V_BE_FAST, V_MC_PERS, V_FAST_LDS, V_COUNT
+    V_MC_FUSE_X, V_ZC_SEQ, V_ZC_NODMA, V_BE_FAST, V_MC_PERS, V_FAST_LDS, V_OCC_LDS, V_COUNT
 };
 int64_t variant(Variant v);                                     // INT64_MIN when unset
 inline bool variant_is(Variant v, int64_t value) { return variant(v) == value; }
 inline bool variant_off(Variant v) { return variant(v) == 0; }                 // set to 0
 inline bool variant_on(Variant v) { const int64_t x = variant(v); return x != INT64_MIN && x != 0; }
 inline int64_t variant_or(Variant v, int64_t dflt) { const int64_t x = variant(v); return x == INT64_MIN ? dflt : x; }
+// variant OCC_LDS: bytes of unused dynamic LDS added to a wave-per-stream launch (occupancy-cap A/B
+// of the memory-bound kernels; 0 / unset = none)
+inline size_t occ_lds() { const int64_t x = variant(V_OCC_LDS); return x > 0 && x <= 65536 ? (size_t)x : 0; }
 
 
 // ---- cross-lane (wave64) helpers: DPP row shifts + row broadcasts (GFX9-family DPP) ----

@@ -700,7 +700,7 @@ __global__ OFS_SCM_BOUNDS void sc_minn_pk_kernel(WinFusedArgs a) {
 template <int MODE, int E, int MW, int NB>
 int launch(const WinFastArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
-    hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+    hipLaunchKernelGGL((win_fast_kernel<MODE, E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), ofs::occ_lds(), st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
@@ -741,9 +741,9 @@ template <int E, int MW, int NB>
 int launch_fused(const WinFusedArgs& a, hipStream_t st) {
     const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
     if (OFS_SCM_PK)
-        hipLaunchKernelGGL((sc_minn_pk_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+        hipLaunchKernelGGL((sc_minn_pk_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), ofs::occ_lds(), st, a);
     else
-        hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), 0, st, a);
+        hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), ofs::occ_lds(), st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
