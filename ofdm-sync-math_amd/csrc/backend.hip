@@ -61,9 +61,27 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 }
 // a / b exactly as numpy divides complex128 (Smith's algorithm with the reciprocal scale
 // scl = 1 / (b.x + b.y * rat), no contraction): bit-identical to numpy on the same operands
+#ifndef OFS_BE_CDIV_SEL
+#define OFS_BE_CDIV_SEL 1          // 0: numpy's two branches as branches (A/B)
+#endif
 __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
 #pragma clang fp contract(off)
     const double br = fabs(b.x), bi = fabs(b.y);
+#if OFS_BE_CDIV_SEL
+    // Branch-free: both of numpy's cases are one formula on swapped operands (the larger |b|
+    // component p, the other q; a's components u, v in the same order), so a wave whose lanes
+    // split between the cases runs ONE pair of fp64 divisions instead of both branches' pairs.
+    // Bit-identical: case 2's real part a.x·rat + a.y = u + v·rat (addition commutes exactly) and
+    // its imaginary part a.y·rat - a.x = -(v - u·rat) (x - y = -(y - x) exactly, then ·scl).
+    // b = 0: numpy's a.x / |b.x|, a.y / |b.y| = a·(+inf) (signed inf, or NaN for a 0 or NaN part).
+    const bool c1 = br >= bi;
+    const double p = c1 ? b.x : b.y, q = c1 ? b.y : b.x;
+    const double u = c1 ? a.x : a.y, v = c1 ? a.y : a.x;
+    const double rat = q / p, scl = 1.0 / (p + q * rat);
+    const double re = (u + v * rat) * scl, t = (v - u * rat) * scl;
+    const bool zero = br == 0.0 && bi == 0.0;
+    return make_double2(zero ? a.x * __builtin_inf() : re, zero ? a.y * __builtin_inf() : (c1 ? t : -t));
+#else
     if (br >= bi) {
         if (br == 0.0 && bi == 0.0) return make_double2(a.x / br, a.y / bi);
         const double rat = b.y / b.x, scl = 1.0 / (b.x + b.y * rat);
@@ -71,6 +89,7 @@ __device__ __forceinline__ double2 cdiv(double2 a, double2 b) {
     }
     const double rat = b.x / b.y, scl = 1.0 / (b.y + b.x * rat);
     return make_double2((a.x * rat + a.y) * scl, (a.y * rat - a.x) * scl);
+#endif
 }
 
 // workgroup barrier ordering LDS only: every barrier here orders LDS traffic (the global inputs
