@@ -425,11 +425,13 @@ int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows,
 /* ROWS plan for the reference's sliding shape (many offsets per stream): one rocFFT execution covers
  * EVERY offset of rows_per_exec consecutive [T]-sample rows (rows = stream x branch; 0 = all
  * total_rows; at execute time a multiple of n_br) - its windows start at sample cp of the first row
- * at a distance of ONE sample, (rows-1)*T + n_off of them, and the store callback keeps the template
- * bins of the windows that lie inside one row (always pruned: prune_bins = n_bins, N a power of two
- * <= 4096).  ofs_zc_freq_metric_fft then issues 2 launches per row group instead of 2 per offset;
- * the spectrum buffer is [ofs_zc_fft_plan_chunk(plan)][prune_bins].  The FFTs cover T instead of
- * n_off windows per row (T / n_off times the per-offset plan's transforms). */
+ * at a distance of ONE sample, (rows-1)*T + n_off of them (N a power of two <= 4096).  prune_bins =
+ * n_bins: the store callback keeps the template bins of the windows that lie inside one row, spectrum
+ * buffer [ofs_zc_fft_plan_chunk(plan)][prune_bins]; prune_bins = 0: no callback (rocFFT's callback
+ * path blocks the host per execution), every window's dense spectrum goes to a
+ * [ofs_zc_fft_plan_chunk(plan)][N] buffer and the gather reads the template bins from it.
+ * ofs_zc_freq_metric_fft then issues 2 launches per row group instead of 2 per offset.  The FFTs
+ * cover T instead of n_off windows per row (T / n_off times the per-offset plan's transforms). */
 int32_t ofs_zc_fft_plan_create_rows(int32_t precision, int32_t N, int32_t cp, int64_t T,
                                     int64_t total_rows, int64_t rows_per_exec, int32_t prune_bins,
                                     void** plan_out, size_t* work_bytes);

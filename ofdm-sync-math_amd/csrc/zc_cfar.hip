@@ -126,6 +126,12 @@ __device__ unsigned zc_hwid[4096 * 8];       // HW_ID of every wave (workgroup-m
 #ifndef OFS_ZC_NT
 #define OFS_ZC_NT 1
 #endif
+// helpers read c from global memory (L2: the walker's DMA brought the rows in) instead of the LDS
+// tile, template HG: taken when state arrays are stored (paired, r06k: state mode 0.564 -> 0.540 ms;
+// events + mask only 0.285 -> 0.342 ms, so not there); OFS_ZC_HGLOBAL = 1 forces it (A/B)
+#ifndef OFS_ZC_HGLOBAL
+#define OFS_ZC_HGLOBAL 0
+#endif
 template <class T>
 __device__ __forceinline__ void zc_st(T* p, T v) {
 #if OFS_ZC_NT
@@ -181,7 +187,7 @@ __device__ __forceinline__ void zc_walk_chunk(const double* x, const double* o, 
     }
 }
 
-template <bool DMA, int ZS, int ZH>
+template <bool DMA, int ZS, int ZH, bool HG>
 __global__ __launch_bounds__(64 * (1 + ZH))
 void zc_cfar_kernel(ZcArgs a) {
 #pragma clang fp contract(off)
@@ -351,7 +357,12 @@ void zc_cfar_kernel(ZcArgs a) {
 #if OFS_ZC_DIAG_NOLDS                                           // diagnostic: no helper LDS reads
                     cv[rr][j] = 1e-3 * (double)(lane + sr) + (double)qc; lv[rr][j] = cv[rr][j] * 1e30;
 #else
-                    cv[rr][j] = tc[qc % NC][sr][64 * rr + lane];
+                    if constexpr (HG || OFS_ZC_HGLOBAL) {
+                        const int64_t ig = (int64_t)qc * ZC + 64 * rr + lane;
+                        cv[rr][j] = ig < n ? cw[(int64_t)sr * n + ig] : 0.0;
+                    } else {
+                        cv[rr][j] = tc[qc % NC][sr][64 * rr + lane];
+                    }
                     lv[rr][j] = ta[qc & 1][sr][64 * rr + lane];
 #endif
                 }
@@ -494,8 +505,11 @@ int ofs_zc_cfar_try(const double* corr_mag, int64_t B, int64_t n, int W, double 
     constexpr int SD = OFS_ZC_S, HD = OFS_ZC_H, SR = OFS_ZC_S_REG, HR = OFS_ZC_H_REG;
     const bool dma = ZC % 128 == 0 && n % ZC == 0 && W % ZC == 0 && W >= 0 &&
                      (reinterpret_cast<uintptr_t>(corr_mag) & 15) == 0 && !ofs::variant_on(ofs::V_ZC_NODMA);
-    if (dma) hipLaunchKernelGGL((zc_cfar_kernel<true, SD, HD>), dim3((unsigned)((B + SD - 1) / SD)), dim3(64 * (1 + HD)), 0, st, a);
-    else hipLaunchKernelGGL((zc_cfar_kernel<false, SR, HR>), dim3((unsigned)((B + SR - 1) / SR)), dim3(64 * (1 + HR)), 0, st, a);
+    const bool state = local_sum || corr_scaled || thresh_scaled;
+    const dim3 gd((unsigned)((B + SD - 1) / SD)), gr((unsigned)((B + SR - 1) / SR));
+    if (dma && state) hipLaunchKernelGGL((zc_cfar_kernel<true, SD, HD, true>), gd, dim3(64 * (1 + HD)), 0, st, a);
+    else if (dma) hipLaunchKernelGGL((zc_cfar_kernel<true, SD, HD, false>), gd, dim3(64 * (1 + HD)), 0, st, a);
+    else hipLaunchKernelGGL((zc_cfar_kernel<false, SR, HR, false>), gr, dim3(64 * (1 + HR)), 0, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 

@@ -126,8 +126,8 @@ __global__ __launch_bounds__(ZWG) void zc_gather_kernel(GatherArgs a) {
     }
 }
 
-// rows plans: metric[b][off] for every offset of the execution's streams from the compact spectrum of
-// windows w = (b·n_br + br)·T + off.  One wave per (stream, offset), lane k = template bin k; the
+// rows plans: metric[b][off] for every offset of the execution's streams from the spectrum of windows
+// w = (b·n_br + br)·T + off: compact [window][n_bins] (pruned plans) or dense [window][N] (no callback).  One wave per (stream, offset), lane k = template bin k; the
 // streams stride over gridDim.y (<= 65535, the launch limit), so any rows-per-execution fits.
 template <class R>
 __global__ __launch_bounds__(ZWG) void zc_gather_rows_kernel(GatherArgs a, int64_t T) {
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(ZWG) void zc_gather_rows_kernel(GatherArgs a, int64
         if (lane < a.n_bins) {
             const double tr = a.t_re[lane], ti = a.t_im[lane];
             for (int br = 0; br < a.n_br; ++br) {
-                const int64_t i = ((b * a.n_br + br) * T + off) * a.n_bins + lane;
+                const int64_t i = ((b * a.n_br + br) * T + off) * a.N + a.pos[lane];   // pruned: N = n_bins, pos = k
                 double xr, xi;
                 if constexpr (sizeof(R) == 4) {
                     const float2 v = reinterpret_cast<const float2*>(a.spec)[i];
@@ -314,8 +314,11 @@ int32_t ofs_zc_fft_plan_create3(int32_t precision, int32_t N, int64_t n_windows,
 
 int32_t ofs_zc_fft_plan_create_rows(int32_t precision, int32_t N, int32_t cp, int64_t T, int64_t total_rows,
                                     int64_t rows_per_exec, int32_t prune_bins, void** plan_out, size_t* work_bytes) {
+    // prune_bins 0: a DENSE rows plan - no store callback, every window's N-point spectrum written to the
+    // caller's [chunk][N] buffer and gathered from there (rocFFT's callback path blocks the host per
+    // execution on a synchronous hipMemcpyFromSymbol)
     if (!plan_out || (precision != OFS_FP32 && precision != OFS_FP64) || N < 1 || cp < 0 || total_rows < 1 ||
-        rows_per_exec < 0 || prune_bins < 1 || prune_bins > ZB || N > 4096 || (N & (N - 1)))
+        rows_per_exec < 0 || prune_bins < 0 || prune_bins > ZB || N > 4096 || (N & (N - 1)))
         return OFS_EINVAL;
     if (T < (int64_t)N + cp) return OFS_ESHORT;
     *plan_out = nullptr;
@@ -345,12 +348,13 @@ int32_t ofs_zc_fft_plan_create_rows(int32_t precision, int32_t N, int32_t cp, in
     p->n_windows = total_rows;
     p->in_dist = T;
     p->prune = prune_bins;
-    bool ok = hipMalloc(&p->cb_dev, sizeof(ZcCbData)) == hipSuccess &&
-              hipHostMalloc(&p->cb_host, sizeof(ZcCbData)) == hipSuccess &&
-              (memset(p->cb_host, 0, sizeof(ZcCbData)), true) &&
-              hipMemcpyFromSymbol(&p->cb_fn, precision == OFS_FP32 ? HIP_SYMBOL(zc_store_cb_f32_ptr)
-                                                                  : HIP_SYMBOL(zc_store_cb_f64_ptr),
-                                  sizeof(void*)) == hipSuccess && p->cb_fn;
+    bool ok = prune_bins == 0 ||
+              (hipMalloc(&p->cb_dev, sizeof(ZcCbData)) == hipSuccess &&
+               hipHostMalloc(&p->cb_host, sizeof(ZcCbData)) == hipSuccess &&
+               (memset(p->cb_host, 0, sizeof(ZcCbData)), true) &&
+               hipMemcpyFromSymbol(&p->cb_fn, precision == OFS_FP32 ? HIP_SYMBOL(zc_store_cb_f32_ptr)
+                                                                   : HIP_SYMBOL(zc_store_cb_f64_ptr),
+                                   sizeof(void*)) == hipSuccess && p->cb_fn);
     if (!ok) {
         if (p->cb_dev) (void)hipFree(p->cb_dev);
         if (p->cb_host) (void)hipHostFree(p->cb_host);

@@ -166,7 +166,8 @@ ROWS_MAX_RATIO = 4                  # ... and only while T <= ROWS_MAX_RATIO x o
 
 
 def rows_per_exec(n_rows: int, n_br: int, T: int, n_bins: int, esz: int) -> int:
-    """Rows per rows-plan execution: a compact spectrum of about ROWS_SPECTRUM_BYTES, whole streams."""
+    """Rows per rows-plan execution: a spectrum (n_bins per window: the template's when pruned, N when
+    dense) of about ROWS_SPECTRUM_BYTES, whole streams."""
     per = max(n_br, (ROWS_SPECTRUM_BYTES // max(1, T * n_bins * esz)) // n_br * n_br)
     return min(per, n_rows)                  # (the gather strides its streams over gridDim.y: no 65535 cap)
 
@@ -207,14 +208,16 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     ``pruned`` (N a power of two <= 4096, distinct bins): rocFFT's store callback keeps only the
     template bins, so no dense spectrum is written (1.03x the algorithmic bytes instead of 2.02x);
     measured 2.3x SLOWER on cfg5 (34.2 vs 15.0 ms: rocFFT's callback kernel calls the store
-    through a function pointer per element), hence off by default.
+    through a function pointer per element, and each execution blocks the host on a synchronous
+    hipMemcpyFromSymbol), hence off by default in both layouts.
     ``chunk``: windows per rocFFT execution (None or 0: one execution over the whole batch;
     ``default_chunk`` sizes one for the Infinity Cache); the spectrum scratch is [chunk][N].  Chunking
     keeps the spectrum round trip on-die but measured neutral on cfg5 (17.5 vs 17.7 ms): rocFFT's
     own 4096-point kernel, not HBM, bounds the leg.
     ``layout``: "offsets" - one rocFFT execution (+ gather) per offset, as above; "rows" - one execution
-    per group of rows covering every offset of them (windows one sample apart, always pruned:
-    ofs_zc_fft_plan_create_rows), 2 launches per row group instead of 2 per offset - the form for the
+    per group of rows covering every offset of them (windows one sample apart, ofs_zc_fft_plan_create_rows;
+    dense spectrum rows, or compact ones through the callback with ``pruned``), 2 launches per row group
+    instead of 2 per offset - the form for the
     reference's own sliding shape (thousands of offsets per stream); "auto": "rows" when the template is
     prunable, ``chunk`` is not given, there are at least ROWS_MIN_OFFSETS offsets per stream and
     T <= ROWS_MAX_RATIO x offsets (the rows plan's extra FFT work, T / offsets, stays small), else
@@ -245,18 +248,19 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
         return out
     prunable = N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
     rows = pick_rows_layout(layout, prunable, chunk, batch.T, noff)
-    pruned = (bool(pruned) or rows) and prunable
+    pruned = bool(pruned) and prunable
     nw = batch.B * batch.nb
     out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)
     pk = torch.empty((batch.B,), dtype=torch.int64, device=dev) if return_peak else None
     pv = torch.empty((batch.B,), dtype=torch.float64, device=dev) if return_peak else None
     if rows:
         esz = 8 if prec == _lib.FP32 else 16
-        rpe = int(rows_per_execution) if rows_per_execution else rows_per_exec(nw, batch.nb, batch.T, int(idx.size), esz)
+        nbin = int(idx.size) if pruned else N               # compact (callback) or dense spectrum rows
+        rpe = int(rows_per_execution) if rows_per_execution else rows_per_exec(nw, batch.nb, batch.T, nbin, esz)
         if rpe % batch.nb:
             raise ValueError("rows_per_execution must be a multiple of the branch count")
-        plan = _plan(prec, N, nw, batch.T, int(idx.size), rpe, rows_cp=cp)
-        spec = torch.empty((plan.chunk, int(idx.size)), dtype=batch.data.dtype, device=dev)
+        plan = _plan(prec, N, nw, batch.T, int(idx.size) if pruned else 0, rpe, rows_cp=cp)
+        spec = torch.empty((plan.chunk, nbin), dtype=batch.data.dtype, device=dev)
         work = torch.empty((max(plan.work_bytes, 1),), dtype=torch.uint8, device=dev) if plan.work_bytes else None
         rc = _lib.lib().ofs_zc_freq_metric_fft(plan.handle, batch.fmt, batch.data.data_ptr(), batch.B, batch.nb,
                                                batch.T, N, cp, int(idx.size), idx.ctypes.data, tb.ctypes.data,

@@ -618,33 +618,58 @@ def zc_freq_refshape(dev, st, steps, warmup, B=4096):
                   B * noff * 62 * (12 * nb + 10), "fp64")
 
 
-def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows"):
+def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows", pruned=False):
     """The north-star rocFFT formulation of zc_freq.compute_frequency_metric (zc_freq.py:62-99: one FFT per
     window) at the reference's own sliding shape (T = 4242, 2 branches, N = 2048, cp = 512: 1683 offsets
     per stream), complex64, B streams.  layout "rows": ofs_zc_fft_plan_create_rows - every offset of a row
-    group in one rocFFT execution (windows one sample apart, pruned by the store callback; T windows per
-    row are transformed for n_off used); "offsets": one execution + gather per offset (2 x 1683 launches
-    per row group).  Bound: the FFT flops (5 N log2 N per transformed window) against the fp32 vector
+    group in one rocFFT execution (windows one sample apart; T windows per row are transformed for n_off
+    used), dense spectrum rows (default) or, with pruned, compact ones through rocFFT's store callback
+    (which blocks the host per execution); "offsets": one execution + gather per offset (2 x 1683
+    launches per row group).  Bound: the FFT flops (5 N log2 N per transformed window) against the fp32 vector
     peak - the sliding DFT (zc_freq_refshape) does O(62) work per offset instead of O(N log N)."""
     T, N, cp, nb = 4242, 2048, 512, 2
     g = torch.Generator(device=dev).manual_seed(8)
     x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    pr = True if layout == "offsets" else pruned
     ms = timed(lambda: zc_freq.compute_frequency_metric_rocfft_batched(x, N=N, cp=cp, layout=layout,
-                                                                       pruned=True), steps, warmup, st)
+                                                                       pruned=pr), steps, warmup, st)
     noff = T - (N + cp) + 1
     windows = B * nb * (T if layout == "rows" else noff)
     fft_flops = windows * 5 * N * 11
-    r = dict(config="zc_freq_refshape_rocfft" + ("" if layout == "rows" else "_offsets"),
+    name = "zc_freq_refshape_rocfft" + ("" if layout == "rows" else "_offsets") + ("_pruned" if layout == "rows" and pr else "")
+    r = dict(config=name,
              workload=f"zc_freq N={N} cp={cp}, {B} x {nb} x {T} c64 -> f32 via rocFFT ({layout} layout)",
-             kernel=("rocFFT fp32 C2C over every offset of a row group per execution (in_dist 1, pruning store "
-                     "callback) + zc_gather_rows_kernel" if layout == "rows" else
+             kernel=("rocFFT fp32 C2C over every offset of a row group per execution (in_dist 1, "
+                     + ("pruning store callback" if pr else "dense spectrum rows, no callback")
+                     + ") + zc_gather_rows_kernel" if layout == "rows" else
                      "per offset: rocFFT fp32 C2C (pruned) + zc_gather_kernel"),
              samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4, transformed_windows=windows,
-             launches_per_call=(2 * -(-B * nb // zc_freq.rows_per_exec(B * nb, nb, T, 62, 8)) if layout == "rows"
-                                else 2 * noff), bytes_per_sample="8 in + 4 out per offset")
+             launches_per_call=(2 * -(-B * nb // zc_freq.rows_per_exec(B * nb, nb, T, 62 if pr else N, 8))
+                                if layout == "rows" else 2 * noff), bytes_per_sample="8 in + 4 out per offset")
     r.update(fft_flops=fft_flops, fft_tflops=round(fft_flops / (ms / 1e3) / 1e12, 2),
              fft_flop_frac_fp32=round(fft_flops / (ms / 1e3) / 157.3e12, 4))
     return r
+
+
+def zc_freq_fewoff_rocfft(dev, st, steps, warmup, B=4096, layout="auto"):
+    """A few-offsets shape for the rocFFT leg's layout choice (advisor, round 5): N = 4096, cp = 0,
+    T = 4103 (8 offsets per stream), one branch, complex64, B streams.  "auto" takes the offsets plan
+    here (T / offsets = 513 > zc_freq.ROWS_MAX_RATIO); "rows" forces the rows plan, which transforms
+    T windows per stream for the 8 used."""
+    T, N, cp, nb = 4103, 4096, 0, 1
+    g = torch.Generator(device=dev).manual_seed(9)
+    x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
+    noff = T - (N + cp) + 1
+    rows = zc_freq.pick_rows_layout(layout, True, None, T, noff)
+    ms = timed(lambda: zc_freq.compute_frequency_metric_rocfft_batched(x, N=N, cp=cp, layout=layout),
+               steps, warmup, st)
+    windows = B * nb * (T if rows else noff)
+    return dict(config="zc_freq_fewoff_rocfft" + ("_rows" if layout == "rows" else ""),
+                workload=f"zc_freq N={N} cp={cp}, {B} x {nb} x {T} c64 -> f32 via rocFFT ({layout} layout -> "
+                         f"{'rows' if rows else 'offsets'})",
+                kernel="rocFFT fp32 C2C + gather", samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4,
+                transformed_windows=windows, fft_flops=windows * 5 * N * 12,
+                bytes_per_sample="8 in + 4 out per offset")
 
 
 def zc_detect(dev, st, steps, warmup, state=False, seq=False):
@@ -674,6 +699,9 @@ CONFIGS = {"zc_mf_direct": lambda *a, **k: zc_mf(*a, method="direct", **k), "par
            "zc_freq_fp64": zc_freq_fp64, "zc_freq_refshape": zc_freq_refshape, "zc_detect": zc_detect,
            "zc_freq_refshape_rocfft": zc_freq_refshape_rocfft,
            "zc_freq_refshape_rocfft_offsets": lambda *a, **k: zc_freq_refshape_rocfft(*a, layout="offsets", **k),
+           "zc_freq_refshape_rocfft_pruned": lambda *a, **k: zc_freq_refshape_rocfft(*a, pruned=True, **k),
+           "zc_freq_fewoff_rocfft": zc_freq_fewoff_rocfft,
+           "zc_freq_fewoff_rocfft_rows": lambda *a, **k: zc_freq_fewoff_rocfft(*a, layout="rows", **k),
            "zc_detect_state": lambda *a, **k: zc_detect(*a, state=True, **k),
            "zc_detect_seq": lambda *a, **k: zc_detect(*a, seq=True, **k),
            "cfg5_rocfft_dense": lambda *a, **k: cfg5_rocfft(*a, pruned=False, **k),
