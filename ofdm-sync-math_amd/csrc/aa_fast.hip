@@ -119,7 +119,11 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
 #endif
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)xcd_block() * (FAST_WG / 64) + w;
+    // block order: one antenna plain blockIdx, two the XCD remap (paired under the occupancy cap,
+    // profiles/r06n_headline_remap_ff_ab.txt: without the remap cfg3 0.2994 -> 0.2940 ms, detect-only
+    // 0.1036 -> 0.0949, T 4096 1.225 -> 1.211; two antennas 0.4004 -> 0.4055 and the 2 x 5315 shape
+    // slower in 2 of 3 rounds - they keep it)
+    const int64_t b = (int64_t)(NA == 1 ? blockIdx.x : xcd_block()) * (FAST_WG / 64) + w;
     if (b >= a.B) return;
     const int T = (int)a.T;
 #if OFS_FAST_STAGE == 0
@@ -215,7 +219,9 @@ __global__ OFS_FAST_BOUNDS void aa_fast_kernel(AaFastArgs a) {
     double Cr[RW + 1], Ci[RW + 1], Ce[RW + 1];  // running row bases (wave-uniform)
     Cr[0] = Ci[0] = Ce[0] = 0.0;
 
-    AaRowGate<E, float, false, (bool)(DO || OFS_FAST_FF)> gate;   // event state (wave-uniform)
+    // scan-free gate flags: detect-only, and the one-antenna storing kernel (round 6, under the occupancy
+    // cap: 0.2905 -> 0.2889 ms, 0.2979 -> 0.2966 with the remap; r06m / r06n)
+    AaRowGate<E, float, false, (bool)(DO || OFS_FAST_FF || NA == 1)> gate;   // event state (wave-uniform)
 #if OFS_FAST_GATE_LATE
     constexpr int GR = RW - MR > 0 ? RW - MR : 1;             // gated rows (k >= MR)
     __shared__ float4 gl[FAST_WG / 64][GR][E][64];            // (M, |P|^2, Re P, Im P) per sample
@@ -568,7 +574,7 @@ __global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
     using S = AaStream<E, MR, NA, DO>;
     __shared__ float4 lagbuf[STREAM_WG / 64][S::LDSLAG ? MR : 1][NA][S::V4][64];
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)xcd_block() * (STREAM_WG / 64) + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)(NA == 1 ? blockIdx.x : xcd_block()) * (STREAM_WG / 64) + (threadIdx.x >> 6);   // (as aa_fast_kernel)
     if (b >= a.B) return;
     S s;
     s.lane = lane;
