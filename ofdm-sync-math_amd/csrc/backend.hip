@@ -118,7 +118,13 @@ __device__ double block_sum(double v, double* red) {
 
 // numpy.mod for float64 (result has the sign of the divisor)
 __device__ __forceinline__ double np_mod(double a, double b) {
-    double m = fmod(a, b);
+    // fmod(a, b) = a - n·b exactly; for b > 0 and |a| < 2b, n is 0 or ±1 and a ∓ b is exact (Sterbenz:
+    // |a| in [b, 2b]), so the library's general fmod (an iterative routine) is needed only beyond that -
+    // the unwrap's a = dd + pi with |dd| <= 2 pi never goes there.  Same bits: a zero result takes the
+    // sign of b below either way.
+    double m;
+    if (b > 0.0 && fabs(a) < 2.0 * b) m = a >= b ? a - b : (a <= -b ? a + b : a);
+    else m = fmod(a, b);
     if (m != 0.0) {
         if ((b < 0.0) != (m < 0.0)) m += b;
     } else {
@@ -683,6 +689,12 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 #ifndef OFS_BE_LDS40
 #define OFS_BE_LDS40 1             // phases and reduction slots inside the sample buffer (0: own LDS, A/B)
 #endif
+#ifndef OFS_BE_MIDSLOTS
+#define OFS_BE_MIDSLOTS 1          // reduction slots over the spectrum's unused Nyquist bins (below)
+#endif
+#ifndef OFS_BE_NOFRAMEBAR
+#define OFS_BE_NOFRAMEBAR 1        // no barrier at the top of the frame loop under L40 (below)
+#endif
 #ifndef OFS_BE_DEARLY
 #define OFS_BE_DEARLY 0
 #endif
@@ -713,8 +725,12 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     // the phases live in the buffer between the pilot's LS and the unwrap (the pilot spectrum is in
     // registers by then), the reduction slots at its end; barriers before each window placement
     // keep the placement's writes behind the last reads of those slots
-    double* ph = reinterpret_cast<double*>(buf);                       // n_used <= 2N - 9·BW/64
-    double* red = reinterpret_cast<double*>(buf) + 2 * N - 9 * (BW / 64);
+    // OFS_BE_MIDSLOTS: the slots at the Nyquist end of the spectrum, buffer entries N/2 .. N/2 + 17 (bins
+    // within [N/2, N/2 + 64) whatever the swizzle: it permutes bits below 6 only), which centered used-bin
+    // sets never reach (the fast path's n_used <= N·5/8): when no used bin lies there (checked once per
+    // workgroup) the EQ block sums need no barrier before their slot writes; 0: at the buffer's end (A/B)
+    double* ph = reinterpret_cast<double*>(buf);                       // n_used <= N (the slots start at N)
+    double* red = reinterpret_cast<double*>(buf) + (OFS_BE_MIDSLOTS ? N : 2 * N - 9 * (BW / 64));
     double* scan_tot = red + 8 * (BW / 64);
 #else
     __shared__ double red[8 * (BW / 64)];
@@ -733,7 +749,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
         twq[R8 ? tsw(j) : j] = make_double2(cs, sn);
     }
     int kb[UPT];                              // this thread's used bins u = tid + BW·j, as X indices
-    double bsum[1] = {0.0};
+    double bsum[2] = {0.0, 0.0};
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
         const int u = threadIdx.x + BW * j;
@@ -741,10 +757,12 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
         k = k < 0 ? k + N : k;
         kb[j] = R8 ? bsw<SPT>(k) : k;                                     // buffer slot of bin k
         if (u < U) bsum[0] += (double)a.bins[u];
+        if (u < U && k >= N / 2 && k < N / 2 + 64) bsum[1] = 1.0;        // a used bin under the mid slots
     }
     // the phase-slope fit's frame-invariant sums (np.mean(k), Σ kz, Σ kz² + 1e-12)
-    block_sums<1>(bsum, rs());
+    block_sums<2>(bsum, rs());
     const double kmean = bsum[0] / (double)U;
+    const bool slots_clear = L40 && OFS_BE_MIDSLOTS && bsum[1] == 0.0;   // EQ sums without the extra barrier
     double kst[2] = {0.0, 0.0};
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
@@ -768,7 +786,10 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
         cpx.issue(a, blockIdx.x, a.pilot_start[blockIdx.x]);
     }
     for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    lds_barrier();
+    // (L40 + OFS_BE_NOFRAMEBAR: no barrier here - the CFO block sums write the other slot set than the
+    // previous frame's last sums, RED2, and the barrier before the pilot window's placement orders every
+    // earlier LDS read behind it)
+    if (!(L40 && OFS_BE_NOFRAMEBAR && OFS_BE_RED2)) lds_barrier();
     const int64_t ps = a.pilot_start[b], ds = a.data_start[b];
     if (!PF) {                        // (CPFIRST: the CFO would wait for the CP samples alone - vmcnt
         if (OFS_BE_CPFIRST) {         // counts in order - with the pilot window's loads still in flight)
@@ -872,7 +893,8 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
             gs[3] += r.x * r.x + r.y * r.y;
         }
     }
-    block_sums<4, L40>(gs, rs());                                     // (L40: the slots overlay the data spectrum)
+    if (slots_clear) block_sums<4, false>(gs, rs());                  // (slots over unused bins only)
+    else block_sums<4, L40>(gs, rs());                                // (L40: the slots overlay the data spectrum)
     const double rr = gs[3];
     BE_T(7)
     const double2 g = cdiv(make_double2(gs[0], gs[1]), make_double2(gs[2] + 1e-12, 0.0));
@@ -1039,7 +1061,8 @@ extern "C" int32_t ofs_rx_backend(int32_t in_fmt, const void* x, int64_t B, int3
                       ((n_fft == 4 * BW && n_used <= 3 * BW) || (n_fft == 8 * BW && n_used <= 5 * BW) ||
                        (n_fft == 16 * BW && n_used <= 10 * BW));
     if (fast) {
-        const size_t lds_f = (size_t)n_fft * 16 + (size_t)(n_fft / 4) * 16 + (OFS_BE_LDS40 ? 0 : (size_t)n_used * 8);
+        const size_t lds_f = (size_t)n_fft * 16 + (size_t)(n_fft / 4) * 16 + (OFS_BE_LDS40 ? 0 : (size_t)n_used * 8) +
+                             ofs::occ_lds();                       // variant OCC_LDS: occupancy A/B only
         auto launch_f = [&](auto kern) -> int32_t {
             if (lds_f > 64 * 1024 &&
                 hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_f) != hipSuccess)
