@@ -97,6 +97,10 @@ const char* ofs_status_string(int32_t status);
  *   ZC_SEQ       1: zc_v2 CFAR + gate through the sequential one-wave-per-stream kernel
  *   ZC_NODMA     1: zc_v2 CFAR tiles through registers instead of LDS-DMA
  *   BE_FAST      0: receiver back-end through the generic kernel
+ *   FAST_LDS     n > 0: bytes of unused dynamic LDS per workgroup of the aa_fast kernel (occupancy
+ *                cap; default 16384 for the one-antenna storing kernel = 10 per CU, 1 = no cap)
+ *   OCC_LDS      n >= 0: bytes of unused dynamic LDS added to the other wave-per-stream launches
+ *                (aa_stream, win_fast, aa_exact, rtl_exact, the fast back-end; occupancy A/B)
  * ofs_debug_set_variant returns OFS_EINVAL for an unknown name; value OFS_VARIANT_UNSET clears
  * one variant, ofs_debug_reset_variants clears all.  The table is per calling thread
  * (thread_local): a variant set by one thread steers only the calls that same thread makes, and

@@ -190,15 +190,16 @@ def test_rocfft_chunk_must_split_branches():
                                                         idx, t, e, N=64, cp=16, chunk=3)
 
 
+@pytest.mark.parametrize("pruned", [False, True])
 @pytest.mark.parametrize("prec,N,cp,T,nb,B,rpe", [("c128", 2048, 512, 4242, 2, 5, 0), ("c128", 2048, 512, 4242, 2, 5, 4),
                                                   ("c64", 2048, 512, 4242, 2, 64, 0), ("c128", 256, 32, 700, 3, 7, 6),
                                                   ("c64", 128, 0, 1000, 1, 33, 5)])
-def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe):
+def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe, pruned):
     """The rows plan (ofs_zc_fft_plan_create_rows: every offset of a row group in ONE rocFFT execution,
-    windows one sample apart, the callback dropping the windows that straddle two rows) gives the
-    per-offset plan's metric and argmax on the reference's own sliding shape (T = 4242, 2 branches,
-    N = 2048, cp = 512: 1683 offsets), with row groups that leave a tail; fp64 also vs the oracle,
-    complex64 within error model 2 on every window."""
+    windows one sample apart; dense spectrum rows by default, or the store callback keeping the template
+    bins of the windows inside one row with pruned=True) gives the per-offset plan's metric and argmax on
+    the reference's own sliding shape (T = 4242, 2 branches, N = 2048, cp = 512: 1683 offsets), with row
+    groups that leave a tail; fp64 also vs the oracle, complex64 within error model 2 on every window."""
     rng = np.random.default_rng(N + T + B)
     x = rng_c(rng, B, nb, T)
     sym = O.pss_symbol(N)
@@ -209,7 +210,7 @@ def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe):
     idx, t, e = O.zc_template()
     xd = torch.from_numpy(x).cuda()
     r, pr, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
-                                                               layout="rows", rows_per_execution=rpe)
+                                                               layout="rows", rows_per_execution=rpe, pruned=pruned)
     o, po, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
                                                                layout="offsets", pruned=True)
     a, b_ = r.cpu().numpy(), o.cpu().numpy()
@@ -221,6 +222,25 @@ def test_rocfft_rows_layout_equals_offsets(prec, N, cp, T, nb, B, rpe):
             np.testing.assert_allclose(a[k], O.zc_freq_metric(x[k], N, cp, idx, t, e), rtol=1e-9, atol=1e-11)
     else:
         st = oracle_c.zc_freq_check(x, N, cp, idx, t, e, a, EM.rocfft_eps(N), 6.0)
-        print(f"rows c64 N={N}: max |dm|/bound {st[:, 1].max():.3g}")
+        print(f"rows c64 N={N} pruned={pruned}: max |dm|/bound {st[:, 1].max():.3g}")
         assert st[:, 1].max() <= 1.0
         np.testing.assert_allclose(a, b_, rtol=1e-5, atol=1e-8)
+
+
+def test_rocfft_rows_execution_beyond_grid_y_limit():
+    """One rows-plan execution over more than 65535 streams: zc_gather_rows_kernel strides its streams
+    over gridDim.y (<= 65535), so the launch still covers every stream (advisor, round 5); the metric
+    equals the per-offset plan's (fp32, different rocFFT plans: within 1e-5), the peaks its own argmax."""
+    N, cp, T, B = 64, 0, 66, 66000
+    rng = np.random.default_rng(5)
+    x = rng_c(rng, B, 1, T).astype(np.complex64)
+    idx, t, e = O.zc_template()
+    xd = torch.from_numpy(x).cuda()
+    r, pr, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                               layout="rows", rows_per_execution=B)
+    o, po, _ = zc_freq.compute_frequency_metric_rocfft_batched(xd, idx, t, e, N=N, cp=cp, return_peak=True,
+                                                               layout="offsets")
+    assert r.shape == (B, T - N - cp + 1)
+    np.testing.assert_allclose(r.cpu().numpy(), o.cpu().numpy(), rtol=1e-5, atol=1e-8)
+    rn = r.cpu().numpy()
+    assert np.array_equal(pr.cpu().numpy(), np.argmax(rn, axis=1))     # every stream's row was written
