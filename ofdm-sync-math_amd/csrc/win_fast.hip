@@ -285,10 +285,17 @@ struct WinFusedArgs {
 #ifndef OFS_SCM_WAVES
 #define OFS_SCM_WAVES 0
 #endif
+// workgroup size of the fused kernels by branch count: two branches run 2 waves (streams) per
+// workgroup - paired (round 6, tools/libs_cfg_ab.sh, profiles/r06t_cfg4_workgroup_ab.txt): cfg4_2br
+// 0.4367 ms at 4 waves, 0.4159 at 2, 0.4225 at 1; one branch (cfg4) keeps 4 (5.30 vs 5.50 / 5.74 ms)
+#ifndef OFS_SCM_WG2
+#define OFS_SCM_WG2 128
+#endif
+constexpr int scm_wg(int nb) { return nb == 2 ? OFS_SCM_WG2 : WF_WG; }
 #if OFS_SCM_WAVES > 0
-#define OFS_SCM_BOUNDS __launch_bounds__(WF_WG, OFS_SCM_WAVES)
+#define OFS_SCM_BOUNDS __launch_bounds__(scm_wg(NB), OFS_SCM_WAVES)
 #else
-#define OFS_SCM_BOUNDS __launch_bounds__(WF_WG)
+#define OFS_SCM_BOUNDS __launch_bounds__(scm_wg(NB))
 #endif
 
 template <int E, int MW, int NB>
@@ -300,10 +307,11 @@ __global__ OFS_SCM_BOUNDS void sc_minn_fast_kernel(WinFusedArgs a) {
     constexpr int PD = 2;
     constexpr int PER = ER;
     constexpr int V4 = E / 2;
-    __shared__ float hist[WF_WG / 64][ER + 2 * XR][E][64];   // [S_e rows | S_q re rows | S_q im rows]
+    constexpr int WG = scm_wg(NB);
+    __shared__ float hist[WG / 64][ER + 2 * XR][E][64];   // [S_e rows | S_q re rows | S_q im rows]
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)xcd_block_w() * (WF_WG / 64) + w;
+    const int64_t b = (int64_t)xcd_block_w() * (WG / 64) + w;
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
@@ -532,11 +540,12 @@ __global__ OFS_SCM_BOUNDS void sc_minn_pk_kernel(WinFusedArgs a) {
     constexpr int PD = 2;
     constexpr int PER = ER;
     constexpr int V4 = E / 2;
-    __shared__ float histE[WF_WG / 64][ER][E][64];     // S_e of the last ER rows
-    __shared__ pf2 histQ[WF_WG / 64][XR][E][64];       // conj S_q of the last XR rows
+    constexpr int WG = scm_wg(NB);
+    __shared__ float histE[WG / 64][ER][E][64];     // S_e of the last ER rows
+    __shared__ pf2 histQ[WG / 64][XR][E][64];       // conj S_q of the last XR rows
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t b = (int64_t)xcd_block_w() * (WF_WG / 64) + w;
+    const int64_t b = (int64_t)xcd_block_w() * (WG / 64) + w;
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int64_t nout = T - N + 1;
@@ -739,11 +748,12 @@ void pick(int W, int& E, int& mw) {
 
 template <int E, int MW, int NB>
 int launch_fused(const WinFusedArgs& a, hipStream_t st) {
-    const int64_t grid = (a.B + WF_WG / 64 - 1) / (WF_WG / 64);
+    constexpr int WG = scm_wg(NB);
+    const int64_t grid = (a.B + WG / 64 - 1) / (WG / 64);
     if (OFS_SCM_PK)
-        hipLaunchKernelGGL((sc_minn_pk_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), ofs::occ_lds(), st, a);
+        hipLaunchKernelGGL((sc_minn_pk_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WG), ofs::occ_lds(), st, a);
     else
-        hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WF_WG), ofs::occ_lds(), st, a);
+        hipLaunchKernelGGL((sc_minn_fast_kernel<E, MW, NB>), dim3((unsigned)grid), dim3(WG), ofs::occ_lds(), st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
