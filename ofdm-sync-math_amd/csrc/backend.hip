@@ -285,10 +285,18 @@ __device__ __attribute__((noinline)) double be_log10(double x) { return log10(x)
 #ifndef OFS_BE_NT
 #define OFS_BE_NT 1
 #endif
+typedef double be_d2v __attribute__((ext_vector_type(2)));
+#ifndef OFS_BE_ST16
+#define OFS_BE_ST16 1              // 0: two 8-byte halves per complex output (A/B)
+#endif
 __device__ __forceinline__ void be_st(double2* p, double2 v) {
 #if OFS_BE_NT
+#if OFS_BE_ST16
+    __builtin_nontemporal_store(be_d2v{v.x, v.y}, reinterpret_cast<be_d2v*>(p));   // one 16-byte store
+#else
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
+#endif
 #else
     *p = v;
 #endif

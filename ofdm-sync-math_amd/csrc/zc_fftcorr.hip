@@ -501,6 +501,10 @@ __device__ __forceinline__ void mp_wave_sync() {
 constexpr int MP_LDS = (MF_M + 512 + 32) * 16 + 8 * 8;   // block, w_8192^t (t < 512), w_512^k (k < 32), wave sums
 // slot of block element e: low four bits XOR bits 4-7 (conflict-free for t + 512m, 512g + 32i + k, 16t + i)
 __device__ __forceinline__ int mp_at(int e) { return e ^ ((e >> 4) & 15); }
+typedef double mp_d2v __attribute__((ext_vector_type(2)));
+#ifndef OFS_MP_ST16
+#define OFS_MP_ST16 1               // 0: two 8-byte halves per complex output (A/B)
+#endif
 // energy prefix P[j] (doubles, in the block region during the extract): one pad per 16
 __device__ __forceinline__ int mp_pq(int j) { return j + (j >> 4); }
 __device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
@@ -832,7 +836,12 @@ __global__ __launch_bounds__(MP_T) void mc_pers_kernel(McArgs a, const double2* 
             const double inv = mp_rsqrt(ewc) * rn_inv;
             const double2 r = make_double2(c.x * inv, c.y * inv);
 #if OFS_MP_NTST                     // tuning builds: non-temporal output stores
+            // (one 16-byte store per complex sample: a 2 x f64 vector, not two 8-byte halves)
+#if OFS_MP_ST16
+            if (a.out && st_ok) __builtin_nontemporal_store(mp_d2v{r.x, r.y}, reinterpret_cast<mp_d2v*>(&a.out[oi]));
+#else
             if (a.out && st_ok) { __builtin_nontemporal_store(r.x, &a.out[oi].x); __builtin_nontemporal_store(r.y, &a.out[oi].y); }
+#endif
             if (a.mag && st_ok) __builtin_nontemporal_store(mp_cabs(r), &a.mag[oi]);
 #else
             if (a.out && st_ok) a.out[oi] = r;

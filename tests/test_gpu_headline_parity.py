@@ -99,3 +99,30 @@ def test_detector_object_equals_batched_function():
         for s in range(256):
             assert torch.equal(a.ev_int[s, :n[s]], b.ev_int[s, :n[s]])
             assert torch.equal(a.ev_real[s, :n[s]], b.ev_real[s, :n[s]])
+
+
+@pytest.mark.parametrize("na,T_", [(1, 1024), (2, 5315)])
+def test_occupancy_cap_changes_no_bit(na, T_, variant):
+    """The occupancy caps (16 KiB of unused LDS per workgroup for the one-antenna storing kernel, a
+    24 KiB workgroup for the two-antenna streaming kernel) change only WHEN streams run, not their
+    arithmetic: P, R, M and the events with the default launch equal those with the caps lifted
+    (variants FAST_LDS = 1, OCC_LDS = 0), bit for bit."""
+    from ofdm_sync_amd import _lib, sync_aa, synth
+    dev = torch.device("cuda", 0)
+    Bc = 20000                                             # > 10 per CU x 256 CUs: several waves of workgroups
+    det = sync_aa.AABatchDetector(Bc, T_, na, L, outputs=("P", "R", "M"), max_events=4, device=dev)
+    base = synth.faded_base(L, "cir1", tuple(range(na)) if na > 1 else (1,))
+    det.x.copy_(synth.synth_batch(base, Bc, T_, seed=77, device=dev))
+    outs = []
+    for cap in (True, False):
+        with _lib.variants(FAST_LDS=None if cap else 1, OCC_LDS=None if cap else 0):
+            r = det.run()
+            torch.cuda.synchronize()
+            outs.append([t.clone() for t in (r.P, r.R, r.M, r.n_events, r.ev_int, r.ev_real)])
+    n = outs[0][3]
+    assert torch.equal(n, outs[1][3])
+    live = sync_aa.live_events(n, 4)
+    for a_, b_ in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a_, b_)
+    for a_, b_ in zip(outs[0][4:], outs[1][4:]):
+        assert torch.equal(a_[live], b_[live])
