@@ -380,10 +380,17 @@ constexpr int STREAM_WG = OFS_STREAM_WG;
 #ifndef OFS_STREAM_WAVES
 #define OFS_STREAM_WAVES 0
 #endif
+// workgroup size of the streaming kernel: the one-antenna storing kernel runs 2 streams per workgroup
+// (round 6, paired, profiles/r06v_stream_kernel_variants_ab.txt: T 4096 1.222 -> 1.192 ms); two
+// antennas (the 2 x 5315 reference shape: 0.578 vs 0.608 ms) and detect-only keep one
+#ifndef OFS_STREAM_WG1
+#define OFS_STREAM_WG1 128
+#endif
+constexpr int stream_wg(int na, bool det_only) { return (na == 1 && !det_only) ? OFS_STREAM_WG1 : STREAM_WG; }
 #if OFS_STREAM_WAVES > 0
-#define OFS_STREAM_BOUNDS __launch_bounds__(STREAM_WG, OFS_STREAM_WAVES)
+#define OFS_STREAM_BOUNDS __launch_bounds__(stream_wg(NA, DO), OFS_STREAM_WAVES)
 #else
-#define OFS_STREAM_BOUNDS __launch_bounds__(STREAM_WG)
+#define OFS_STREAM_BOUNDS __launch_bounds__(stream_wg(NA, DO))
 #endif
 
 #ifndef OFS_STREAM_FF
@@ -572,9 +579,10 @@ struct AaStream {
 template <int E, int MR, int NA, bool DO>
 __global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
     using S = AaStream<E, MR, NA, DO>;
-    __shared__ float4 lagbuf[STREAM_WG / 64][S::LDSLAG ? MR : 1][NA][S::V4][64];
+    constexpr int SWG = stream_wg(NA, DO);
+    __shared__ float4 lagbuf[SWG / 64][S::LDSLAG ? MR : 1][NA][S::V4][64];
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)(NA == 1 ? blockIdx.x : xcd_block()) * (STREAM_WG / 64) + (threadIdx.x >> 6);   // (as aa_fast_kernel)
+    const int64_t b = (int64_t)(NA == 1 ? blockIdx.x : xcd_block()) * (SWG / 64) + (threadIdx.x >> 6);   // (as aa_fast_kernel)
     if (b >= a.B) return;
     S s;
     s.lane = lane;
@@ -621,7 +629,8 @@ __global__ OFS_STREAM_BOUNDS void aa_stream_kernel(AaFastArgs a) {
 template <int E, int MR, int NA>
 int launch_stream(const AaFastArgs& a, hipStream_t st) {
     const bool det_only = a.detect && !a.P && !a.R && !a.M && !a.valid;
-    const int64_t grid = (a.B + STREAM_WG / 64 - 1) / (STREAM_WG / 64);
+    constexpr int WGD = stream_wg(NA, true), WGS = stream_wg(NA, false);
+    const int64_t grid = det_only ? (a.B + WGD / 64 - 1) / (WGD / 64) : (a.B + WGS / 64 - 1) / (WGS / 64);
     // occupancy cap of the two-antenna storing kernel: 24 KiB of LDS per workgroup in all (unused
     // dynamic LDS on top of its 8 KiB lag ring at L 512) = 6 workgroups per CU.  Paired on the
     // reference's detector shape (16384 x 2 x 5315, L 512; 3 rounds, profiles/r06g_occupancy_sweeps.txt):
@@ -629,14 +638,14 @@ int launch_stream(const AaFastArgs& a, hipStream_t st) {
     // (~27 KiB per workgroup rounds up past 160 KiB / 6: 5 per CU); one antenna at T = 4096 is faster
     // uncapped (1.186 vs 1.228 ms).  variant OCC_LDS (bytes added) overrides.
     using S = AaStream<E, MR, NA, false>;
-    constexpr size_t lag_lds = (size_t)(STREAM_WG / 64) * (S::LDSLAG ? MR : 1) * NA * S::V4 * 64 * 16;
+    constexpr size_t lag_lds = (size_t)(WGS / 64) * (S::LDSLAG ? MR : 1) * NA * S::V4 * 64 * 16;
     constexpr size_t cap_total = 24 * 1024;
     const size_t dflt = (!det_only && NA == 2 && cap_total > lag_lds) ? cap_total - lag_lds : 0;
     const size_t shm = ofs::variant(ofs::V_OCC_LDS) == INT64_MIN ? dflt : ofs::occ_lds();
     if (det_only)
-        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(STREAM_WG), shm, st, a);
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, true>), dim3((unsigned)grid), dim3(WGD), shm, st, a);
     else
-        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(STREAM_WG), shm, st, a);
+        hipLaunchKernelGGL((aa_stream_kernel<E, MR, NA, false>), dim3((unsigned)grid), dim3(WGS), shm, st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 
