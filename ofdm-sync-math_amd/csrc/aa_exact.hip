@@ -35,6 +35,14 @@ constexpr int XW = 256;                 // 4 waves = 4 streams per workgroup
 #define OFS_XPD1 4
 #endif
 constexpr int XA = OFS_XA_WG;           // aa_exact_kernel workgroup (tuning builds: 64)
+// workgroup of one instantiation: the integer L = RL one-antenna kernel (cfg2a) runs one stream per
+// workgroup - paired (round 6, profiles/r06y_exact_wg_ab.txt): cfg2a 0.0283 -> 0.0273 ms, packed AXIS
+// words 0.0322 -> 0.0313; complex128 keeps 4 (cfg3_fp64 0.5895 vs 0.6106 ms at 1, the 2 x 5315 fp64
+// shape 1.1348 vs 1.1473)
+#ifndef OFS_XA_WG_I1
+#define OFS_XA_WG_I1 64
+#endif
+constexpr int xa_wg(int fmt, int mr, int na) { return (fmt != OFS_C128 && mr == 1 && na == 1) ? OFS_XA_WG_I1 : XA; }
 
 // E consecutive int16 I/Q words (packed (I, Q) in one int32) of one lane, zero past T
 template <int E>
@@ -170,7 +178,7 @@ struct RowPrefixI {
 // valid = n >= L; M = min(|P|²/R², 1) if valid and R > 1e-6·L else 0 (sync_aa.py:458-493).
 // ------------------------------------------------------------------------------------------
 template <int FMT, int E, int MR, int NA>
-__global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : (FMT != OFS_C128 && MR == 1 && NA == 1 ? OFS_XWPE1 : 1)) void aa_exact_kernel(AaFastArgs a) {
+__global__ __launch_bounds__(xa_wg(FMT, MR, NA), (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : (FMT != OFS_C128 && MR == 1 && NA == 1 ? OFS_XWPE1 : 1)) void aa_exact_kernel(AaFastArgs a) {
     using X = XSamp<FMT == OFS_CP12 ? OFS_CI16 : FMT>;          // CP12 decodes to int16 I/Q words
     using W = typename X::W;
     constexpr int RL = 64 * E;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(XA, (FMT == OFS_C128 && MR == 4 && NA == 1) ? 2 : (
     constexpr int PD = (FMT != OFS_C128 && MR == 1 && NA == 1) ? OFS_XPD1 : (E <= 2 ? 4 : 2);   // rows in flight ahead of use
     constexpr int PER = MR > PD ? MR : PD;                   // unroll period (MR, PD powers of 2)
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)xcd_block_w() * (XA / 64) + (threadIdx.x >> 6);
+    const int64_t b = (int64_t)xcd_block_w() * (xa_wg(FMT, MR, NA) / 64) + (threadIdx.x >> 6);
     if (b >= a.B) return;
     const int64_t T = a.T;
     const int nrows = (int)((T + RL - 1) / RL);
@@ -869,11 +877,11 @@ bool exact_enabled() {                  // variant EXACT=0 forces the general en
 template <int E, int MR, int NA>
 int aa_launch(int fmt, const AaFastArgs& a, hipStream_t st) {
     if (fmt == OFS_C128)
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_C128, E, MR, NA>), dim3((unsigned)((a.B + xa_wg(OFS_C128, MR, NA) / 64 - 1) / (xa_wg(OFS_C128, MR, NA) / 64))), dim3(xa_wg(OFS_C128, MR, NA)), ofs::occ_lds(), st, a);
     else if (fmt == OFS_CP12)
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_CP12, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CP12, E, MR, NA>), dim3((unsigned)((a.B + xa_wg(OFS_CP12, MR, NA) / 64 - 1) / (xa_wg(OFS_CP12, MR, NA) / 64))), dim3(xa_wg(OFS_CP12, MR, NA)), ofs::occ_lds(), st, a);
     else
-        hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + XA / 64 - 1) / (XA / 64))), dim3(XA), ofs::occ_lds(), st, a);
+        hipLaunchKernelGGL((aa_exact_kernel<OFS_CI16, E, MR, NA>), dim3((unsigned)((a.B + xa_wg(OFS_CI16, MR, NA) / 64 - 1) / (xa_wg(OFS_CI16, MR, NA) / 64))), dim3(xa_wg(OFS_CI16, MR, NA)), ofs::occ_lds(), st, a);
     return hipGetLastError() == hipSuccess ? 1 : OFS_EHIP;
 }
 template <int E, int MR>
