@@ -249,7 +249,8 @@ def kernel_label(plan: int) -> str:
     if plan >= 1000:
         e, mr = (plan - 1000) // 10, (plan - 1000) % 10
         kind = "streaming" if plan >= 1100 else "register-staged"
-        return f"aa_fast_kernel<E={e},MR={mr}> (wave per stream, {kind}, fused metric + events)"
+        cap = ", 10 workgroups per CU" if plan < 1100 else ""
+        return f"aa_fast_kernel<E={e},MR={mr}> (wave per stream, {kind}, fused metric + events{cap})"
     return {1: "win_kernel<C64,fp32,AA> (fused events)", 2: "win_kernel<C64,fp32,AA> + aa_events_kernel"}.get(plan, str(plan))
 
 

@@ -61,6 +61,33 @@ __global__ __launch_bounds__(256) void pattern_wave(const float4* __restrict__ x
     }
 }
 
+// pattern_wave with one wave (= one stream) per 64-thread workgroup: the round-6 headline geometry,
+// launched with unused dynamic LDS to cap the workgroups per CU as the headline does (16 KiB = 10)
+template <int T>
+__global__ __launch_bounds__(64) void pattern_wave1(const float4* __restrict__ x, float4* __restrict__ P,
+                                                   float4* __restrict__ R, float4* __restrict__ M, int64_t B) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = blockIdx.x;
+    if (b >= B) return;
+    constexpr int RW = T / 256;
+    float4 v[RW][2];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const int64_t q = (b * T + 256 * k + 4 * lane) / 2;
+        v[k][0] = x[q]; v[k][1] = x[q + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const int64_t s = b * T + 256 * k + 4 * lane;
+        P[s / 2] = v[k][0]; P[s / 2 + 1] = v[k][1];
+        const float4 a = v[k][0], c = v[k][1];
+        const float4 r = make_float4(a.x * a.x + a.y * a.y, a.z * a.z + a.w * a.w, c.x * c.x + c.y * c.y,
+                                     c.z * c.z + c.w * c.w);
+        R[s / 4] = r;
+        M[s / 4] = make_float4(r.x * 0.5f, r.y * 0.5f, r.z * 0.5f, r.w * 0.5f);
+    }
+}
+
 // pattern_wave with the headline kernel's shape of a wave's life: the stream DMA'd into LDS
 // (global_load_lds_dwordx4), then per row a dependent VALU chain of NV ops (standing in for the
 // metric arithmetic) before the row's stores
@@ -215,6 +242,10 @@ int main(int argc, char** argv) {
            time_ms([&] { pattern_flat<<<(unsigned)((n / 4 + 255) / 256), 256>>>(x, P, R, M, n / 4); }, iters));
     report("pattern_wave(8r+16w) wave-per-stream", 24.0 * n,
            time_ms([&] { pattern_wave<1024><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
+    for (int pad : {0, 13000, 14800, 16384, 18000, 20480}) {
+        snprintf(nm, sizeof nm, "pattern_wave1(8r+16w) 64-thread wg, LDS pad %d", pad);
+        report(nm, 24.0 * n, time_ms([&] { pattern_wave1<1024><<<(unsigned)B, 64, pad>>>(x, P, R, M, B); }, iters));
+    }
     report("pattern_lds<NV=0>", 24.0 * n,
            time_ms([&] { pattern_lds<1024, 0><<<(unsigned)((B + 3) / 4), 256>>>(x, P, R, M, B); }, iters));
     report("pattern_lds<NV=64>", 24.0 * n,
