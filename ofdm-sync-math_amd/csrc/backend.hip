@@ -583,7 +583,7 @@ __device__ __forceinline__ double2 twq_sw(const double2* twq, int ti, bool upper
 // their order (bit-identical to fft_lds), one LDS round trip and one barrier per log2 R stages.
 // p and i·h have disjoint bits, as have k·str and q·h·str (k < h), so every address is a
 // per-thread swizzled base XOR a compile-time constant.
-template <int R, int SPT>
+template <int R, int SPT, bool WSYNC = false>
 __device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int h) {
     constexpr int N = SPT * BW, Q = N / 4, LQ = __builtin_ctz(Q);
     for (int j = be_tid(); j < N / R; j += BW) {
@@ -616,7 +616,13 @@ __device__ __forceinline__ void fft_pass(double2* buf, const double2* twq, int h
 #pragma unroll
         for (int i = 0; i < R; ++i) buf[pb ^ bsw<SPT>(i * h)] = v[i];
     }
-    lds_barrier();
+    if constexpr (WSYNC) {                 // the next pass reads only what this wave wrote (fft_rest)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        lds_barrier();
+    }
 }
 
 template <int B>
@@ -678,9 +684,16 @@ __device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, dou
     lds_barrier();
 }
 
+// OFS_BE_WSYNC: for SPT <= 8 the first pass hands over to the second wave-locally - pass 1 thread j
+// writes the 8·SPT elements of group j / SPT, pass 2 thread j reads the 64·SPT elements of group
+// G = j / (8·SPT), which pass-1 threads [8·SPT·G, 8·SPT·(G + 1)) wrote: 64 (SPT 8) or 32 (SPT 4)
+// threads of j's own wave (SPT 16: 128 threads, two waves - barrier)
+#ifndef OFS_BE_WSYNC
+#define OFS_BE_WSYNC 1
+#endif
 template <int SPT>
 __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
-    fft_pass<8, SPT>(buf, twq, SPT);
+    fft_pass<8, SPT, OFS_BE_WSYNC && SPT <= 8>(buf, twq, SPT);
     fft_pass<8, SPT>(buf, twq, 8 * SPT);
     fft_pass<4, SPT>(buf, twq, 64 * SPT);
 }
