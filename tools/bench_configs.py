@@ -618,7 +618,7 @@ def zc_freq_refshape(dev, st, steps, warmup, B=4096):
                   B * noff * 62 * (12 * nb + 10), "fp64")
 
 
-def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows", pruned=False):
+def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows", pruned=False, rpe=0):
     """The north-star rocFFT formulation of zc_freq.compute_frequency_metric (zc_freq.py:62-99: one FFT per
     window) at the reference's own sliding shape (T = 4242, 2 branches, N = 2048, cp = 512: 1683 offsets
     per stream), complex64, B streams.  layout "rows": ofs_zc_fft_plan_create_rows - every offset of a row
@@ -631,8 +631,9 @@ def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows", pruned
     g = torch.Generator(device=dev).manual_seed(8)
     x = torch.randn((B, nb, T), dtype=torch.complex64, device=dev, generator=g)
     pr = True if layout == "offsets" else pruned
+    kw = {"rows_per_execution": rpe} if (layout == "rows" and rpe) else {}
     ms = timed(lambda: zc_freq.compute_frequency_metric_rocfft_batched(x, N=N, cp=cp, layout=layout,
-                                                                       pruned=pr), steps, warmup, st)
+                                                                       pruned=pr, **kw), steps, warmup, st)
     noff = T - (N + cp) + 1
     windows = B * nb * (T if layout == "rows" else noff)
     fft_flops = windows * 5 * N * 11
@@ -644,8 +645,9 @@ def zc_freq_refshape_rocfft(dev, st, steps, warmup, B=256, layout="rows", pruned
                      + ") + zc_gather_rows_kernel" if layout == "rows" else
                      "per offset: rocFFT fp32 C2C (pruned) + zc_gather_kernel"),
              samples=B * nb * T, ms=ms, alg_bytes=B * nb * T * 8 + B * noff * 4, transformed_windows=windows,
-             launches_per_call=(2 * -(-B * nb // zc_freq.rows_per_exec(B * nb, nb, T, 62 if pr else N, 8))
-                                if layout == "rows" else 2 * noff), bytes_per_sample="8 in + 4 out per offset")
+             launches_per_call=(2 * -(-B * nb // (rpe or zc_freq.rows_per_exec(B * nb, nb, T, 62 if pr else N, 8)))
+                                if layout == "rows" else 2 * noff), rows_per_execution=rpe or None,
+             bytes_per_sample="8 in + 4 out per offset")
     r.update(fft_flops=fft_flops, fft_tflops=round(fft_flops / (ms / 1e3) / 1e12, 2),
              fft_flop_frac_fp32=round(fft_flops / (ms / 1e3) / 157.3e12, 4))
     return r
