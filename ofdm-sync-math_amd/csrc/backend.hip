@@ -547,6 +547,63 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
     return (sv[1] - pmean * skz) / den;
 }
 
+// The same fit with ONE pass over each thread's run and ONE barrier: phi(u) = raw(u) + C_t + lrun(u),
+// C_t the exclusive prefix (over threads) of the thread totals of the unwrap corrections, lrun the
+// thread's own running corrections, so  Σ phi = Σ_t (A_t + C_t·n_t)  and  Σ kz·phi = Σ_t (D_t + C_t·K_t)
+// with A_t = Σ (raw + lrun), D_t = Σ kz·(raw + lrun), K_t = Σ kz, n_t = count over the thread's bins.
+// Within a wave C_t = c_t (DPP exclusive scan) + P_w (the earlier waves' totals): each wave publishes
+// (Σ A_t + c_t n_t, Σ D_t + c_t K_t, its correction total, Σ n_t, Σ K_t) and every thread combines the
+// BW/64 records in wave order.  The sums associate differently from unwrap_slope_fast (slope / STO may
+// differ in the last bits; the unwrap itself is the same np.unwrap per bin).  OFS_BE_UNWRAP1 = 0: the
+// two-barrier form (A/B).
+#ifndef OFS_BE_UNWRAP1
+#define OFS_BE_UNWRAP1 1
+#endif
+__device__ double unwrap_slope_1b(const double* ph, const int32_t* bins, int U, double kmean, double skz, double den,
+                                  double* red, double* kslot) {
+    const int per = (U + BW - 1) / BW;
+    const int u0 = be_tid() * per, u1 = min(U, u0 + per);
+    double lrun = 0.0, A = 0.0, D = 0.0, K = 0.0, cnt = 0.0;
+    double prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
+    for (int u = u0; u < u1; ++u) {
+        const double raw = ph[u];
+        if (u >= 1) {
+            const double dd = raw - prev_raw;
+            if (!(fabs(dd) < M_PI)) {
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                lrun += dm - dd;
+            }
+        }
+        prev_raw = raw;
+        const double p = raw + lrun, kz = (double)bins[u] - kmean;
+        A += p;
+        D += kz * p;
+        K += kz;
+        cnt += 1.0;
+    }
+    const int lane = be_tid() & 63, w = be_tid() >> 6;
+    const double c = ofs::scan_add(lrun) - lrun;            // exclusive wave prefix of the thread totals
+    double v[5] = {A + c * cnt, D + c * K, lrun, cnt, K};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v[i] = ofs::scan_add(v[i]);  // lane 63: the wave's totals
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[w * 4 + i] = v[i];
+        kslot[w] = v[4];
+    }
+    lds_barrier();
+    double sphi = 0.0, skzphi = 0.0, pw = 0.0;
+#pragma unroll
+    for (int k = 0; k < BW / 64; ++k) {
+        sphi += red[k * 4 + 0] + pw * red[k * 4 + 3];
+        skzphi += red[k * 4 + 1] + pw * kslot[k];
+        pw += red[k * 4 + 2];
+    }
+    const double pmean = sphi / (double)U;
+    return (skzphi - pmean * skz) / den;
+}
+
 #ifndef OFS_BE_MINWG
 #define OFS_BE_MINWG 4             // workgroups per CU the register budget is cut for (128 VGPRs, with
                                    // the 40 KB LDS layout, OFS_BE_LDS40).  r05ab: with the lean atan2 /
@@ -877,7 +934,8 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     }
     lds_barrier();
     BE_T(3)
-    const double slope = unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot);
+    const double slope = (OFS_BE_UNWRAP1 && OFS_BE_RED2) ? unwrap_slope_1b(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot)
+                                                         : unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot);
     if (be_tid() == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
         if (a.sto_out) a.sto_out[b] = -slope * (double)N / (2.0 * M_PI);
