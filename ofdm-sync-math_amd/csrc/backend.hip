@@ -774,8 +774,8 @@ __device__ __forceinline__ void fft_rest(double2* buf, const double2* twq) {
 #define OFS_BE_NOFRAMEBAR 1        // no barrier at the top of the frame loop under L40 (below)
 #endif
 #ifndef OFS_BE_DEARLY
-#define OFS_BE_DEARLY 0
-#endif
+#define OFS_BE_DEARLY 2            // data window loads early: 0 never, 1 always, 2 for SPT >= 16 (N 4096: 2 workgroups
+#endif                             // per CU, registers to spare; r06aj 0.825 -> 0.813 ms; N 2048 / 1024 slower)
 #ifndef OFS_BE_CPFIRST
 #define OFS_BE_CPFIRST 0           // 1: CP loads issued before the pilot window's (A/B, r05au: 0.712 vs 0.709 ms
 #endif                             // at N 2048, 0.831 vs 0.818 at 1024, 0.895 vs 0.898 at 4096 - off)
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     BeCp<FMT, NBT> cpx;
     // the data window's loads: issued right after the pilot window is placed (DEARLY: their HBM
     // latency hides under the pilot FFT, LS and unwrap; 32 VGPRs held meanwhile) or just before use
-    constexpr bool DEARLY = OFS_BE_DEARLY && R8;
+    constexpr bool DEARLY = (OFS_BE_DEARLY == 1 || (OFS_BE_DEARLY == 2 && SPT >= 16)) && R8;
     BeWindow<FMT, SPT, NBT> dwin;
     if (PF && blockIdx.x < a.B) {
         pwin.issue(a, blockIdx.x, a.pilot_start[blockIdx.x] + a.cp);
