@@ -172,18 +172,24 @@ def rows_per_exec(n_rows: int, n_br: int, T: int, n_bins: int, esz: int) -> int:
     return min(per, n_rows)                  # (the gather strides its streams over gridDim.y: no 65535 cap)
 
 
-def pick_rows_layout(layout: str, prunable: bool, chunk, T: int, n_off: int) -> bool:
-    """True when compute_frequency_metric_rocfft_batched takes the rows plan: layout "rows", or "auto"
-    with a prunable template, no ``chunk`` (it counts windows of the offsets layout), at least
-    ROWS_MIN_OFFSETS offsets and T <= ROWS_MAX_RATIO x n_off."""
+def pick_rows_layout(layout: str, prunable: bool, chunk, T: int, n_off: int, rows_per_execution=None) -> bool:
+    """True when compute_frequency_metric_rocfft_batched takes the rows plan: layout "rows"; or "auto"
+    with ``rows_per_execution`` given (it sizes only the rows plan); or "auto" with a prunable template,
+    no ``chunk`` (it counts windows of the offsets layout), at least ROWS_MIN_OFFSETS offsets and
+    T <= ROWS_MAX_RATIO x n_off.  Each size argument is refused where its layout is not the one taken."""
     if layout not in ("auto", "offsets", "rows"):
         raise ValueError("layout must be 'auto', 'offsets' or 'rows'")
-    if layout == "rows" and not prunable:
-        raise ValueError("layout='rows' needs a prunable template (N a power of two <= 4096, distinct bins)")
-    if layout == "rows" and chunk:
+    if chunk and rows_per_execution:
+        raise ValueError("chunk (offsets layout) and rows_per_execution (rows layout) exclude each other")
+    if layout == "offsets" and rows_per_execution:
+        raise ValueError("layout='offsets' takes chunk; rows_per_execution sizes the rows layout")
+    rows = layout == "rows" or (layout == "auto" and (bool(rows_per_execution) or (
+        prunable and chunk is None and n_off >= ROWS_MIN_OFFSETS and T <= ROWS_MAX_RATIO * n_off)))
+    if rows and not prunable:
+        raise ValueError("the rows layout needs a prunable template (N a power of two <= 4096, distinct bins)")
+    if rows and chunk:
         raise ValueError("layout='rows' takes rows_per_execution; chunk counts windows of the offsets layout")
-    return layout == "rows" or (layout == "auto" and prunable and chunk is None and n_off >= ROWS_MIN_OFFSETS
-                                and T <= ROWS_MAX_RATIO * n_off)
+    return rows
 
 
 def default_chunk(n_windows: int, n_br: int, N: int, esz: int) -> int:
@@ -222,8 +228,8 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
     prunable, ``chunk`` is not given, there are at least ROWS_MIN_OFFSETS offsets per stream and
     T <= ROWS_MAX_RATIO x offsets (the rows plan's extra FFT work, T / offsets, stays small), else
     "offsets".  ``rows_per_execution``: rows (stream x branch) per rows-plan execution (None or 0:
-    ``rows_per_exec`` sizes a ~256 MiB compact spectrum); ``chunk`` is the offsets layout's windows per
-    execution and is refused with layout="rows"."""
+    ``rows_per_exec`` sizes a ~256 MiB spectrum; given under "auto", it selects the rows layout); ``chunk``
+    is the offsets layout's windows per execution: each is refused with the other layout."""
     if bin_indices is None:
         bin_indices, template_bins, template_energy = make_pss_frequency_template()
     batch = _lib.as_batch(x, batched=True)
@@ -247,7 +253,7 @@ def compute_frequency_metric_rocfft_batched(x, bin_indices=None, template_bins=N
                     torch.empty((0,), dtype=torch.float64, device=dev))
         return out
     prunable = N <= 4096 and (N & (N - 1)) == 0 and len(set(idx.tolist())) == idx.size
-    rows = pick_rows_layout(layout, prunable, chunk, batch.T, noff)
+    rows = pick_rows_layout(layout, prunable, chunk, batch.T, noff, rows_per_execution)
     pruned = bool(pruned) and prunable
     nw = batch.B * batch.nb
     out = torch.empty((batch.B, noff), dtype=torch.float32 if prec == _lib.FP32 else torch.float64, device=dev)

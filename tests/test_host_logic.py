@@ -113,7 +113,8 @@ def test_rocfft_auto_layout_prices_the_rows_plan():
     """layout="auto" takes the rows plan only where its extra FFT work (about T / offsets) is small:
     the reference's sliding shape (T 4242, N 2048 + cp 512: 1683 offsets) yes; few offsets on a long
     row (N 4096, cp 0, T 4103: 8 offsets, ~500x the FFTs) no; never when chunk (windows of the
-    offsets layout) is given; layout="rows" refuses chunk and unprunable templates."""
+    offsets layout) is given; rows_per_execution (the rows layout's size) selects rows under auto and is
+    refused with "offsets"; the rows layout refuses chunk and unprunable templates."""
     pick = zc_freq.pick_rows_layout
     assert pick("auto", True, None, 4242, 4242 - 2560 + 1)
     assert not pick("auto", True, None, 4103, 8)
@@ -122,9 +123,13 @@ def test_rocfft_auto_layout_prices_the_rows_plan():
     assert not pick("auto", True, None, 100, 7)                       # below ROWS_MIN_OFFSETS
     assert pick("auto", True, None, 4 * 1000, 1000) and not pick("auto", True, None, 4 * 1000 + 1, 1000)
     assert pick("rows", True, None, 4103, 8) and not pick("offsets", True, None, 4242, 1683)
+    assert pick("auto", True, None, 4103, 8, rows_per_execution=4)     # the rows-only size selects rows
     for bad in (dict(layout="rows", prunable=True, chunk=64), dict(layout="rows", prunable=False, chunk=None),
-                dict(layout="dense", prunable=True, chunk=None)):
+                dict(layout="dense", prunable=True, chunk=None),
+                dict(layout="offsets", prunable=True, chunk=None, rows_per_execution=4),
+                dict(layout="auto", prunable=True, chunk=64, rows_per_execution=4),
+                dict(layout="auto", prunable=False, chunk=None, rows_per_execution=4)):
         with pytest.raises(ValueError):
-            pick(bad["layout"], bad["prunable"], bad["chunk"], 4242, 1683)
+            pick(bad["layout"], bad["prunable"], bad["chunk"], 4242, 1683, bad.get("rows_per_execution"))
     assert zc_freq.rows_per_exec(10, 2, 4242, 62, 8) == 10
     assert zc_freq.rows_per_exec(1 << 20, 2, 4242, 62, 8) % 2 == 0
