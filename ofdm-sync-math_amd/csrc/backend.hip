@@ -695,17 +695,27 @@ template <> struct Log2<1> { static constexpr int value = 0; };
 // samples n = t + BW·m sit at bit-reversed positions rev(t)·SPT + rev(m): one whole group of the
 // h = 1 pass, so those stages (twiddles w^{q·N/(2s)}) need no LDS round trip; the remaining 8
 // stages run as radix-8, radix-8, radix-4 passes (fft_rest).
+// the tone's per-BW-samples step e^{i·w0·BW/fs}: the same for both windows of a frame, so computed once
+// per frame (OFS_BE_STEP1; 0: per window, A/B) - the same expression, the same bits
+#ifndef OFS_BE_STEP1
+#define OFS_BE_STEP1 1
+#endif
+__device__ __forceinline__ double2 be_tone_step(const BeArgs& a, double cfo) {
+    const double w0 = 2.0 * M_PI * (-cfo);
+    double ss, cc;
+    ofs_bemath::sincos_lean(w0 * (double)BW / a.fs, &ss, &cc);
+    return make_double2(cc, ss);
+}
 template <int FMT, int SPT, int NBT>
 __device__ __forceinline__ void place_window_fft(const BeArgs& a, int64_t s, double cfo,
                                                  const BeWindow<FMT, SPT, NBT>& win, double2* buf,
-                                                 const double2* twq) {
+                                                 const double2* twq, double2 step_in) {
     constexpr int N = SPT * BW, LS = Log2<SPT>::value;
     const double w0 = 2.0 * M_PI * (-cfo);
-    double sn, cs, ss, cc;
+    double sn, cs;
     ofs_bemath::sincos_lean(w0 * (double)(s + (int64_t)be_tid()) / a.fs, &sn, &cs);   // core.apply_cfo's phase
-    ofs_bemath::sincos_lean(w0 * (double)BW / a.fs, &ss, &cc);
     double2 tone = make_double2(cs, sn);
-    const double2 step = make_double2(cc, ss);
+    const double2 step = OFS_BE_STEP1 ? step_in : be_tone_step(a, cfo);
     double2 v[SPT];
 #pragma unroll
     for (int m = 0; m < SPT; ++m) {
@@ -895,13 +905,14 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
         cfo = -ofs_bemath::atan2_lean(pp[1], pp[0]) * a.fs / (2.0 * M_PI * (double)N);
     }
     if (a.cfo_out && be_tid() == 0) a.cfo_out[b] = cfo;
+    const double2 tstep = OFS_BE_STEP1 && R8 ? be_tone_step(a, cfo) : make_double2(0.0, 0.0);
     const double2* pil = a.pilot + b * a.pilot_stride;
     const double2* dat = a.data + b * a.data_stride;
     BE_T(0)
     // ---- pilot: FFT, used bins, LS estimate ----
     if constexpr (L40) lds_barrier();                                 // the CFO sums' slots are read
     if constexpr (R8) {
-        place_window_fft<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, twq);
+        place_window_fft<FMT, SPT, NBT>(a, ps + a.cp, cfo, pwin, buf, twq, tstep);
         if constexpr (DEARLY) dwin.issue(a, b, ds + a.cp);
         BE_T(1)
         fft_rest<SPT>(buf, twq);
@@ -945,7 +956,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     {
         if constexpr (!DEARLY) dwin.issue(a, b, ds + a.cp);
         if constexpr (L40) lds_barrier();                             // the fit sums' slots are read
-        if constexpr (R8) place_window_fft<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, twq);
+        if constexpr (R8) place_window_fft<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, twq, tstep);
         else place_window<FMT, SPT, NBT>(a, ds + a.cp, cfo, dwin, buf, LB);
     }
     if (PF && b + gridDim.x < a.B) {                           // the next frame's pilot window and
