@@ -559,8 +559,45 @@ __device__ double unwrap_slope_fast(const double* ph, const int32_t* bins, int U
 #ifndef OFS_BE_UNWRAP1
 #define OFS_BE_UNWRAP1 1
 #endif
+// OFS_BE_WTOT: the records' bin counts and Σ kz are frame-invariant, so each wave's totals are scanned
+// once per workgroup (be_wave_totals: the same scans of the same values, the same bits) and held as
+// wave-uniform scalars; per frame only the three frame-dependent totals are scanned and published
+#ifndef OFS_BE_WTOT
+#define OFS_BE_WTOT 1
+#endif
+struct BeWaveTot { double n[BW / 64], k[BW / 64]; };
+__device__ __forceinline__ double be_uniform(double v) {
+    const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v)), hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+// each thread's run [u0, u1) as unwrap_slope_1b splits it; its count and Σ kz (the same loop order),
+// scanned per wave, exchanged through LDS (slots: 2·(BW/64) doubles, callers bracket with barriers)
+__device__ BeWaveTot be_wave_totals(const int32_t* bins, int U, double kmean, double* slots) {
+    const int per = (U + BW - 1) / BW;
+    const int u0 = be_tid() * per, u1 = min(U, u0 + per);
+    double K = 0.0, cnt = 0.0;
+    for (int u = u0; u < u1; ++u) {
+        K += (double)bins[u] - kmean;
+        cnt += 1.0;
+    }
+    const double sc = ofs::scan_add(cnt), sk = ofs::scan_add(K);
+    const int lane = be_tid() & 63, w = be_tid() >> 6;
+    if (lane == 63) {
+        slots[w * 2 + 0] = sc;
+        slots[w * 2 + 1] = sk;
+    }
+    lds_barrier();
+    BeWaveTot t;
+#pragma unroll
+    for (int k = 0; k < BW / 64; ++k) {
+        t.n[k] = be_uniform(slots[k * 2 + 0]);
+        t.k[k] = be_uniform(slots[k * 2 + 1]);
+    }
+    lds_barrier();
+    return t;
+}
 __device__ double unwrap_slope_1b(const double* ph, const int32_t* bins, int U, double kmean, double skz, double den,
-                                  double* red, double* kslot) {
+                                  double* red, double* kslot, const BeWaveTot& wt) {
     const int per = (U + BW - 1) / BW;
     const int u0 = be_tid() * per, u1 = min(U, u0 + per);
     double lrun = 0.0, A = 0.0, D = 0.0, K = 0.0, cnt = 0.0;
@@ -584,20 +621,21 @@ __device__ double unwrap_slope_1b(const double* ph, const int32_t* bins, int U, 
     }
     const int lane = be_tid() & 63, w = be_tid() >> 6;
     const double c = ofs::scan_add(lrun) - lrun;            // exclusive wave prefix of the thread totals
+    constexpr int NV = OFS_BE_WTOT ? 3 : 5;
     double v[5] = {A + c * cnt, D + c * K, lrun, cnt, K};
 #pragma unroll
-    for (int i = 0; i < 5; ++i) v[i] = ofs::scan_add(v[i]);  // lane 63: the wave's totals
+    for (int i = 0; i < NV; ++i) v[i] = ofs::scan_add(v[i]);  // lane 63: the wave's totals
     if (lane == 63) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[w * 4 + i] = v[i];
-        kslot[w] = v[4];
+        for (int i = 0; i < (OFS_BE_WTOT ? 3 : 4); ++i) red[w * 4 + i] = v[i];
+        if (!OFS_BE_WTOT) kslot[w] = v[4];
     }
     lds_barrier();
     double sphi = 0.0, skzphi = 0.0, pw = 0.0;
 #pragma unroll
     for (int k = 0; k < BW / 64; ++k) {
-        sphi += red[k * 4 + 0] + pw * red[k * 4 + 3];
-        skzphi += red[k * 4 + 1] + pw * kslot[k];
+        sphi += red[k * 4 + 0] + pw * (OFS_BE_WTOT ? wt.n[k] : red[k * 4 + 3]);
+        skzphi += red[k * 4 + 1] + pw * (OFS_BE_WTOT ? wt.k[k] : kslot[k]);
         pw += red[k * 4 + 2];
     }
     const double pmean = sphi / (double)U;
@@ -863,6 +901,8 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     }
     block_sums<2>(kst, rs());
     const double skz = kst[0], kden = kst[1] + 1e-12;
+    // (the slots: the reduction slot set rs() would hand out next, free until the frame loop)
+    const BeWaveTot wtot = OFS_BE_WTOT ? be_wave_totals(a.bins, U, kmean, red + (rp ^ 1) * 4 * (BW / 64)) : BeWaveTot{};
     BeWindow<FMT, SPT, NBT> pwin;
     BeCp<FMT, NBT> cpx;
     // the data window's loads: issued right after the pilot window is placed (DEARLY: their HBM
@@ -945,7 +985,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     }
     lds_barrier();
     BE_T(3)
-    const double slope = (OFS_BE_UNWRAP1 && OFS_BE_RED2) ? unwrap_slope_1b(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot)
+    const double slope = (OFS_BE_UNWRAP1 && OFS_BE_RED2) ? unwrap_slope_1b(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot, wtot)
                                                          : unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot);
     if (be_tid() == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
