@@ -596,12 +596,51 @@ __device__ BeWaveTot be_wave_totals(const int32_t* bins, int U, double kmean, do
     lds_barrier();
     return t;
 }
+// OFS_BE_UNRW: the run's loop unrolled to its compile-time bound (runs are <= UPT bins) with every
+// phase and bin index read up front; the same operations in the same order, bit-identical.  0: the
+// runtime loop; 1: unrolled; 2 (default): unrolled for runs of 8+ bins (N 4096, 2 workgroups per CU:
+// 0.8057 -> 0.8017 ms; at N 2048 / 1024 slower, 0.6407 -> 0.6478 / 0.7560 -> 0.7632, r06aq)
+#ifndef OFS_BE_UNRW
+#define OFS_BE_UNRW 2
+#endif
+template <int MAXPER>
 __device__ double unwrap_slope_1b(const double* ph, const int32_t* bins, int U, double kmean, double skz, double den,
                                   double* red, double* kslot, const BeWaveTot& wt) {
     const int per = (U + BW - 1) / BW;
     const int u0 = be_tid() * per, u1 = min(U, u0 + per);
     double lrun = 0.0, A = 0.0, D = 0.0, K = 0.0, cnt = 0.0;
     double prev_raw = u0 >= 1 && u0 < U ? ph[u0 - 1] : 0.0;
+    constexpr bool UNR = OFS_BE_UNRW == 1 || (OFS_BE_UNRW == 2 && MAXPER >= 8);
+    if constexpr (UNR) {
+    double rv[MAXPER];
+    int bv[MAXPER];
+#pragma unroll
+    for (int i = 0; i < MAXPER; ++i) {
+        const int u = u0 + i;
+        rv[i] = u < u1 ? ph[u] : 0.0;
+        bv[i] = u < u1 ? bins[u] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < MAXPER; ++i) {
+        const int u = u0 + i;
+        if (u >= u1) break;
+        const double raw = rv[i];
+        if (u >= 1) {
+            const double dd = raw - prev_raw;
+            if (!(fabs(dd) < M_PI)) {
+                double dm = np_mod(dd + M_PI, 2.0 * M_PI) - M_PI;
+                if (dm == -M_PI && dd > 0.0) dm = M_PI;
+                lrun += dm - dd;
+            }
+        }
+        prev_raw = raw;
+        const double p = raw + lrun, kz = (double)bv[i] - kmean;
+        A += p;
+        D += kz * p;
+        K += kz;
+        cnt += 1.0;
+    }
+    } else {
     for (int u = u0; u < u1; ++u) {
         const double raw = ph[u];
         if (u >= 1) {
@@ -618,6 +657,7 @@ __device__ double unwrap_slope_1b(const double* ph, const int32_t* bins, int U, 
         D += kz * p;
         K += kz;
         cnt += 1.0;
+    }
     }
     const int lane = be_tid() & 63, w = be_tid() >> 6;
     const double c = ofs::scan_add(lrun) - lrun;            // exclusive wave prefix of the thread totals
@@ -985,7 +1025,7 @@ __global__ __launch_bounds__(BW, SPT >= 16 ? 2 : (SPT <= 4 ? OFS_BE_MINWG4 : OFS
     }
     lds_barrier();
     BE_T(3)
-    const double slope = (OFS_BE_UNWRAP1 && OFS_BE_RED2) ? unwrap_slope_1b(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot, wtot)
+    const double slope = (OFS_BE_UNWRAP1 && OFS_BE_RED2) ? unwrap_slope_1b<UPT>(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot, wtot)
                                                          : unwrap_slope_fast(ph, a.bins, U, kmean, skz, kden, rs(), scan_tot);
     if (be_tid() == 0) {
         if (a.slope_out) a.slope_out[b] = slope;
